@@ -1,0 +1,182 @@
+/*
+ * ksmcmf.h — C-ABI of the MI355X-native min-cost max-flow solver that replaces
+ * ksched's Flowlessly round-trip (the `placement.Solver` hot path).
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * ksched tree, scheduling/flow/…):
+ *
+ *   ks_create / ks_destroy   placement/solver.go:49-55 NewSolver, :92-109 startSolver
+ *                            (the exec'd flow_scheduler child becomes a device context)
+ *   ks_load_graph            placement/solver.go:111-116 writeGraph → dimacs/export.go:11-29
+ *                            (full "p/n/a" DIMACS text export becomes an array upload)
+ *   ks_apply_deltas          placement/solver.go:118-123 writeIncremental →
+ *                            dimacs/export.go:31-38 + the GenerateChange methods of
+ *                            dimacs/{add_node,create_arc,update_arc,remove_node}_change.go
+ *   ks_solve                 the external Flowlessly solve (solver.go:30-34, Dockerfile:10-12)
+ *                            — min-cost flow, bit-exact total cost and flow value
+ *   ks_get_flows             the "f src dst flow" lines read by readFlowGraph
+ *                            (placement/solver.go:134-179); only arcs with flow > 0
+ *   ks_get_task_mapping      parseFlowToMapping + addPUToSourceNodes
+ *                            (placement/solver.go:183-269) → flowmanager.TaskMapping
+ *                            (flowmanager/types.go:6)
+ *   ks_last_error            the panics of solver.go:97-108, 148-153, 175-178, 223-225
+ *                            become status codes + a message
+ *
+ * Semantics (flowgraph/graph.go:25-41, arc.go:26-36, node.go:76-106):
+ *   - node ids are ksched NodeIDs (dense from 1, reused FIFO after removal,
+ *     graph.go:169-182); excess is the node supply (tasks +1, sink −#tasks);
+ *     type is the DIMACS node type code of export.go:56-68 (task 1, PU 2,
+ *     sink 3, machine 4, numa/socket/cache/core 5, other 0).
+ *   - arcs are (src, dst, low, cap, cost, type); at most one arc per ordered
+ *     (src, dst) pair (node.go:118-131). ADD_ARC on an existing pair upserts.
+ *   - UPDATE_ARC with low == cap == 0 keeps a zero-capacity arc (ChangeArc,
+ *     graph_change_manager.go:142-156; DeleteArc emits the same record,
+ *     :184-193) — an arc with zero capacity carries no flow either way.
+ *   - REMOVE_NODE drops every incident arc implicitly (the reference emits only
+ *     "r id", graph_change_manager.go:129-139); the id may be reused later.
+ *   - SET_EXCESS sets a node's supply explicitly (the sink's demand drifts in
+ *     the reference without a message: graph_manager.go:640, 808). With
+ *     ks_opts.auto_sink != 0 (default) the sink's demand is recomputed as
+ *     −Σ(other supplies) at every solve, which is what keeps an incremental
+ *     DIMACS stream balanced.
+ *
+ * Ownership: input arrays belong to the caller and are copied during the call.
+ * Output buffers are caller-allocated; call with cap = 0 to get the count.
+ * One context per thread; calls on one context are not reentrant
+ * (placement/solver.go:59). Contexts on different devices may run concurrently.
+ */
+#ifndef KSMCMF_H
+#define KSMCMF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSMCMF_ABI_VERSION 1
+
+/* status codes (0 = OK) */
+#define KS_OK            0
+#define KS_E_INVALID    (-1)  /* bad argument / malformed graph or delta          */
+#define KS_E_INFEASIBLE (-2)  /* supplies cannot be routed to the demands         */
+#define KS_E_DEVICE     (-3)  /* HIP runtime error or device not available        */
+#define KS_E_VERIFY     (-4)  /* on-device verification of the result failed      */
+#define KS_E_RANGE      (-5)  /* value outside the solver's integer range         */
+
+/* DIMACS node-type codes (dimacs/add_node_change.go:27-36, export.go:56-68) */
+#define KS_NODE_OTHER    0
+#define KS_NODE_TASK     1
+#define KS_NODE_PU       2
+#define KS_NODE_SINK     3
+#define KS_NODE_MACHINE  4
+#define KS_NODE_INTERMEDIATE 5
+
+typedef struct ks_ctx ks_ctx;
+
+typedef struct ks_opts {
+    int32_t  alpha;            /* cost-scaling factor per ε-phase (default 16)          */
+    int32_t  verify;           /* run the on-device verifier after every solve (1)      */
+    int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */
+    int32_t  sweeps_per_batch; /* push/relabel sweeps per host check (default 32)       */
+    int32_t  gu_interval;      /* sweeps between global price updates (default 48)      */
+    int32_t  reserved[11];
+} ks_opts;
+
+typedef struct ks_node {       /* one "n id excess type" line                            */
+    uint64_t id;
+    int64_t  excess;
+    int32_t  type;
+    int32_t  _pad;
+} ks_node;
+
+typedef struct ks_arc {        /* one "a src dst low cap cost [type]" line               */
+    uint64_t src, dst;
+    uint64_t low, cap;
+    int64_t  cost;
+    int32_t  type;             /* flowgraph.ArcType: 0 other, 1 running (arc.go:18-23)   */
+    int32_t  _pad;
+} ks_arc;
+
+enum ks_delta_kind {
+    KS_ADD_NODE    = 0,        /* "n id excess type"                                     */
+    KS_REMOVE_NODE = 1,        /* "r id"                                                 */
+    KS_ADD_ARC     = 2,        /* "a src dst low cap cost type" (upsert)                 */
+    KS_UPDATE_ARC  = 3,        /* "x src dst low cap cost type oldcost"                  */
+    KS_SET_EXCESS  = 4         /* explicit supply change (sink drift)                    */
+};
+
+typedef struct ks_delta {
+    int32_t  kind;             /* enum ks_delta_kind                                     */
+    int32_t  type;             /* node type (ADD_NODE) or arc type (ADD/UPDATE_ARC)      */
+    uint64_t id;               /* node id (ADD_NODE, REMOVE_NODE, SET_EXCESS)            */
+    uint64_t src, dst;         /* arc endpoints (ADD_ARC, UPDATE_ARC)                    */
+    uint64_t low, cap;
+    int64_t  cost;
+    int64_t  old_cost;         /* UPDATE_ARC only (informational, as in the "x" line)    */
+    int64_t  excess;           /* ADD_NODE, SET_EXCESS                                   */
+} ks_delta;
+
+#define KS_N_PHASE_TIMERS 6    /* build, refine, sweeps, global-update, verify, total    */
+
+typedef struct ks_result {
+    int64_t  total_cost;       /* Σ flow·cost over all arcs (lower bounds included)      */
+    int64_t  flow_value;       /* units routed from supply nodes to demand nodes         */
+    int32_t  status;           /* same code as the ks_solve return value                 */
+    int32_t  phases;           /* ε-phases executed                                      */
+    uint64_t sweeps;           /* push/relabel sweep kernels that did work               */
+    uint64_t arc_scans;        /* residual-arc scans (device counter)                    */
+    uint64_t node_visits;      /* active-node discharges (device counter)                */
+    uint64_t pushes;
+    uint64_t relabels;
+    uint64_t global_updates;
+    uint64_t gu_iterations;    /* Bellman-Ford relaxation rounds inside global updates   */
+    uint64_t gu_arc_scans;     /* residual-arc scans inside global updates               */
+    double   ms_phase[KS_N_PHASE_TIMERS];
+    int64_t  n_nodes;          /* node slots on device                                   */
+    int64_t  n_arcs;           /* live input arcs                                        */
+    uint64_t sweep_launches;   /* k_sweep kernel launches (incl. early-exited ones)      */
+    double   ms_sweep_kernels; /* event-timed span of all sweep batches                   */
+    uint64_t gu_launches;      /* k_gu_relax kernel launches                              */
+    double   ms_gu_kernels;    /* event-timed span of all relaxation batches              */
+} ks_result;
+
+typedef struct ks_flow {       /* one "f src dst flow" line                              */
+    uint64_t src, dst;
+    int64_t  flow;
+} ks_flow;
+
+int         ks_abi_version(void);
+void        ks_default_opts(ks_opts* opts);
+ks_ctx*     ks_create(int device, const ks_opts* opts);
+void        ks_destroy(ks_ctx* ctx);
+const char* ks_last_error(ks_ctx* ctx);
+
+/* Replace the whole graph (first Solve: solver.go:63-83). */
+int ks_load_graph(ks_ctx* ctx, const ks_node* nodes, size_t n,
+                  const ks_arc* arcs, size_t m);
+
+/* Apply a delta stream in mutation order (later Solves: solver.go:86-88). */
+int ks_apply_deltas(ks_ctx* ctx, const ks_delta* deltas, size_t k);
+
+/* Solve min-cost flow on the current graph. result may be NULL. */
+int ks_solve(ks_ctx* ctx, ks_result* result);
+
+/* Arcs with positive flow from the last solve (the "f" lines). */
+int ks_get_flows(ks_ctx* ctx, ks_flow* out, size_t cap, size_t* count);
+
+/* task NodeID → PU NodeID for every task whose unit reaches a PU (TaskMapping). */
+int ks_get_task_mapping(ks_ctx* ctx, uint64_t* task, uint64_t* pu,
+                        size_t cap, size_t* count);
+
+/* Device-resident mapping for RCCL gathers: for the i-th task node in id order
+ * writes the PU node id it maps to, or 0 when unscheduled. dev_out is a device
+ * pointer with room for `cap` uint64; *count receives the number of task nodes. */
+int ks_get_task_pu_device(ks_ctx* ctx, uint64_t* dev_out, size_t cap, size_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KSMCMF_H */

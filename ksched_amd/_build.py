@@ -1,0 +1,47 @@
+"""Build libksmcmf.so in-tree for gfx950 (hipcc, no JIT cache)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libksmcmf.so")
+SOURCES = [os.path.join(CSRC, "ks_engine.hip"), os.path.join(CSRC, "ks_host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "ks_engine.h"), os.path.join(ROOT, "include", "ksmcmf.h")]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm 7.x required)")
+
+
+def stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not stale():
+        return LIB
+    arch = os.environ.get("KS_OFFLOAD_ARCH", "gfx950")
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"),
+           *SOURCES, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,51 @@
+// ks_engine.h — device engine of libksmcmf (gfx950). Internal to the library:
+// the public boundary is include/ksmcmf.h.
+//
+// The engine owns one solve's device state: the input arc arrays (uploaded by
+// the host graph store), the residual CSR built from them on device, the
+// node state (excess, double-buffered prices) and the control block the host
+// polls between kernel batches. See DESIGN.md §3-§4 for the algorithm.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ksmcmf.h"
+
+namespace ks {
+
+struct EngineImpl;
+
+class Engine {
+public:
+    Engine();
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    int init(int device, const ks_opts& opts, std::string& err);
+
+    // Copy a compacted graph (0-based node slots) into device input arrays.
+    // supply[n] is the node excess after any auto-sink adjustment.
+    int upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
+               const int64_t* low, const int64_t* cap, const int64_t* cost,
+               const int64_t* supply, std::string& err);
+
+    // Build the residual CSR on device and run ε-scaling push-relabel to
+    // optimality, then verify on device. Fills r (never NULL here).
+    int solve(ks_result& r, std::string& err);
+
+    // Flow on every input arc (input order) from the last successful solve.
+    int download_flows(int64_t* flows, std::string& err);
+
+    // Copy host bytes to a caller-provided device pointer on the engine stream.
+    int copy_to_device(void* dev_dst, const void* host_src, size_t bytes, std::string& err);
+
+    int device() const;
+
+private:
+    EngineImpl* p_;
+};
+
+}  // namespace ks

@@ -1,0 +1,431 @@
+// ks_host.cpp — host runtime and C-ABI of libksmcmf (include/ksmcmf.h).
+//
+// Mirrors the reference's solver boundary, scheduling/flow/placement/solver.go:
+//   ks_create         ↔ NewSolver (:49-55) + startSolver (:92-109)
+//   ks_load_graph     ↔ writeGraph → dimacs.Export (:111-116, dimacs/export.go:11-29)
+//   ks_apply_deltas   ↔ writeIncremental → dimacs.ExportIncremental (:118-123)
+//   ks_solve          ↔ the Flowlessly solve
+//   ks_get_flows      ↔ the "f" lines consumed by readFlowGraph (:134-179)
+//   ks_get_task_mapping ↔ parseFlowToMapping (:183-269)
+// The graph store keeps ksched's node/arc semantics (flowgraph/graph.go:27-182):
+// NodeIDs index node slots directly, at most one arc per (src, dst), REMOVE_NODE
+// drops incident arcs. The device engine (ks_engine.hip) solves the compacted graph.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ksmcmf.h"
+#include "ks_engine.h"
+
+namespace {
+
+struct NodeRec {
+    int64_t excess = 0;
+    int32_t type = 0;
+    bool alive = false;
+};
+
+struct ArcRec {
+    uint64_t src = 0, dst = 0;
+    int64_t low = 0, cap = 0, cost = 0;
+    int32_t type = 0;
+    bool alive = false;
+};
+
+constexpr uint64_t kMaxId = (1ULL << 30);
+
+inline uint64_t arc_key(uint64_t s, uint64_t d) { return (s << 32) | d; }
+
+}  // namespace
+
+struct ks_ctx {
+    ks::Engine eng;
+    ks_opts opts{};
+    std::string err;
+
+    std::vector<NodeRec> nodes;            // index = NodeID (slot 0 unused)
+    std::vector<ArcRec> arcs;
+    std::vector<int> free_arcs;
+    std::unordered_map<uint64_t, int> arc_of;
+    std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy)
+    bool dirty = true;
+
+    // last upload (compact arrays) and solve outputs
+    std::vector<int> up_arc;               // compact index → arc slot
+    std::vector<int32_t> c_src, c_dst;
+    std::vector<int64_t> c_low, c_cap, c_cost, c_supply;
+    std::vector<int64_t> flows;
+    bool have_solution = false;
+    bool flows_fresh = false;
+    int64_t n_slots = 0;
+
+    int fail(int code, const std::string& msg) {
+        err = msg;
+        return code;
+    }
+};
+
+namespace {
+
+void ensure_node(ks_ctx* c, uint64_t id) {
+    if (id >= c->nodes.size()) {
+        c->nodes.resize(id + 1);
+        c->inc.resize(id + 1);
+    }
+}
+
+bool node_alive(const ks_ctx* c, uint64_t id) { return id < c->nodes.size() && c->nodes[id].alive; }
+
+void kill_arc(ks_ctx* c, int slot) {
+    ArcRec& a = c->arcs[slot];
+    if (!a.alive) return;
+    a.alive = false;
+    c->arc_of.erase(arc_key(a.src, a.dst));
+    c->free_arcs.push_back(slot);
+}
+
+int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int64_t cost, int32_t type) {
+    if (!node_alive(c, s) || !node_alive(c, d))
+        return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has a missing endpoint");
+    if (s == d) return c->fail(KS_E_INVALID, "self-loop arc at node " + std::to_string(s));
+    if (low < 0 || cap < 0 || low > cap)
+        return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has low > cap");
+    if (cap > (int64_t(1) << 53) || cost > (int64_t(1) << 40) || cost < -(int64_t(1) << 40))
+        return c->fail(KS_E_RANGE, "arc capacity or cost outside the supported range");
+    auto it = c->arc_of.find(arc_key(s, d));
+    int slot;
+    if (it != c->arc_of.end()) {
+        slot = it->second;
+    } else {
+        if (!c->free_arcs.empty()) {
+            slot = c->free_arcs.back();
+            c->free_arcs.pop_back();
+        } else {
+            slot = (int)c->arcs.size();
+            c->arcs.emplace_back();
+        }
+        c->arc_of.emplace(arc_key(s, d), slot);
+        c->inc[s].push_back(slot);
+        c->inc[d].push_back(slot);
+    }
+    ArcRec& a = c->arcs[slot];
+    a.src = s;
+    a.dst = d;
+    a.low = low;
+    a.cap = cap;
+    a.cost = cost;
+    a.type = type;
+    a.alive = true;
+    return KS_OK;
+}
+
+int add_node(ks_ctx* c, uint64_t id, int64_t excess, int32_t type) {
+    if (id == 0 || id >= kMaxId) return c->fail(KS_E_RANGE, "node id " + std::to_string(id) + " out of range");
+    ensure_node(c, id);
+    if (c->nodes[id].alive)
+        return c->fail(KS_E_INVALID, "node " + std::to_string(id) + " already present");  // graph.go:95-98
+    c->nodes[id] = NodeRec{excess, type, true};
+    return KS_OK;
+}
+
+int remove_node(ks_ctx* c, uint64_t id) {
+    if (!node_alive(c, id)) return c->fail(KS_E_INVALID, "remove of missing node " + std::to_string(id));
+    for (int slot : c->inc[id]) {
+        const ArcRec& a = c->arcs[slot];
+        if (a.alive && (a.src == id || a.dst == id)) kill_arc(c, slot);
+    }
+    c->inc[id].clear();
+    c->nodes[id] = NodeRec{};
+    return KS_OK;
+}
+
+// Compact the live graph into device input arrays (node slot = id − 1).
+int upload(ks_ctx* c) {
+    uint64_t maxid = 0;
+    for (uint64_t id = c->nodes.size(); id-- > 1;)
+        if (c->nodes[id].alive) {
+            maxid = id;
+            break;
+        }
+    const int64_t n = (int64_t)maxid;
+    c->n_slots = n;
+    c->c_supply.assign(n, 0);
+    int64_t others = 0;
+    int64_t sink = -1, nsinks = 0;
+    for (int64_t v = 0; v < n; ++v) {
+        const NodeRec& r = c->nodes[v + 1];
+        if (!r.alive) continue;
+        c->c_supply[v] = r.excess;
+        if (r.type == KS_NODE_SINK) {
+            sink = v;
+            ++nsinks;
+        } else {
+            others += r.excess;
+        }
+    }
+    if (c->opts.auto_sink && nsinks == 1) c->c_supply[sink] = -others;
+    c->up_arc.clear();
+    c->c_src.clear();
+    c->c_dst.clear();
+    c->c_low.clear();
+    c->c_cap.clear();
+    c->c_cost.clear();
+    for (int slot = 0; slot < (int)c->arcs.size(); ++slot) {
+        const ArcRec& a = c->arcs[slot];
+        if (!a.alive) continue;
+        c->up_arc.push_back(slot);
+        c->c_src.push_back((int32_t)(a.src - 1));
+        c->c_dst.push_back((int32_t)(a.dst - 1));
+        c->c_low.push_back(a.low);
+        c->c_cap.push_back(a.cap);
+        c->c_cost.push_back(a.cost);
+    }
+    const int64_t m = (int64_t)c->up_arc.size();
+    int rc = c->eng.upload(n, m, c->c_src.data(), c->c_dst.data(), c->c_low.data(), c->c_cap.data(),
+                           c->c_cost.data(), c->c_supply.data(), c->err);
+    if (rc == KS_OK) c->dirty = false;
+    return rc;
+}
+
+int fetch_flows(ks_ctx* c) {
+    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
+    if (c->flows_fresh) return KS_OK;
+    c->flows.assign(c->up_arc.size(), 0);
+    int rc = c->eng.download_flows(c->flows.data(), c->err);
+    if (rc == KS_OK) c->flows_fresh = true;
+    return rc;
+}
+
+// Path decomposition of the flow: follow each task's unit along positive-flow
+// arcs (the scheduling network is a DAG) and record the last PU it crosses.
+// Equivalent to parseFlowToMapping (solver.go:183-269) up to the choice among
+// equal-flow decompositions, and correct for mixed-depth DAGs.
+void task_mapping(ks_ctx* c, std::vector<uint64_t>& task, std::vector<uint64_t>& pu) {
+    const int64_t n = c->n_slots, m = (int64_t)c->up_arc.size();
+    std::vector<int> ofirst(n + 2, 0);
+    for (int64_t i = 0; i < m; ++i)
+        if (c->flows[i] > 0) ofirst[c->c_src[i] + 1]++;
+    for (int64_t v = 0; v < n; ++v) ofirst[v + 1] += ofirst[v];
+    std::vector<int> pos(ofirst.begin(), ofirst.end());
+    std::vector<int> odst(ofirst[n] + 1);
+    std::vector<int64_t> orem(ofirst[n] + 1);
+    for (int64_t i = 0; i < m; ++i)
+        if (c->flows[i] > 0) {
+            const int k = pos[c->c_src[i]]++;
+            odst[k] = c->c_dst[i];
+            orem[k] = c->flows[i];
+        }
+    std::vector<int> cur(ofirst.begin(), ofirst.end());
+    task.clear();
+    pu.clear();
+    for (int64_t t = 0; t < n; ++t) {
+        const NodeRec& r = c->nodes[t + 1];
+        if (!r.alive || r.type != KS_NODE_TASK) continue;
+        int64_t v = t, last_pu = -1;
+        for (int64_t steps = 0; steps <= n; ++steps) {
+            if (c->nodes[v + 1].type == KS_NODE_PU) last_pu = v;
+            int k = cur[v];
+            while (k < ofirst[v + 1] && orem[k] == 0) ++k;
+            cur[v] = k;
+            if (k >= ofirst[v + 1]) break;
+            --orem[k];
+            v = odst[k];
+        }
+        if (last_pu >= 0) {
+            task.push_back((uint64_t)t + 1);
+            pu.push_back((uint64_t)last_pu + 1);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ks_abi_version(void) { return KSMCMF_ABI_VERSION; }
+
+void ks_default_opts(ks_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->alpha = 16;
+    o->verify = 1;
+    o->auto_sink = 1;
+    o->sweeps_per_batch = 32;
+    o->gu_interval = 48;
+}
+
+ks_ctx* ks_create(int device, const ks_opts* opts) {
+    ks_ctx* c = new (std::nothrow) ks_ctx;
+    if (!c) return nullptr;
+    if (opts) c->opts = *opts;
+    else ks_default_opts(&c->opts);
+    std::string err;
+    if (c->eng.init(device, c->opts, err) != KS_OK) {
+        delete c;
+        return nullptr;
+    }
+    c->nodes.resize(1);
+    c->inc.resize(1);
+    return c;
+}
+
+void ks_destroy(ks_ctx* c) { delete c; }
+
+const char* ks_last_error(ks_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs, size_t m) {
+    if (!c) return KS_E_INVALID;
+    if ((n && !nodes) || (m && !arcs)) return c->fail(KS_E_INVALID, "null input array");
+    c->nodes.assign(1, NodeRec{});
+    c->inc.assign(1, {});
+    c->arcs.clear();
+    c->free_arcs.clear();
+    c->arc_of.clear();
+    c->arc_of.reserve(m * 2 + 16);
+    c->arcs.reserve(m);
+    c->have_solution = false;
+    c->dirty = true;
+    for (size_t i = 0; i < n; ++i) {
+        int rc = add_node(c, nodes[i].id, nodes[i].excess, nodes[i].type);
+        if (rc) return rc;
+    }
+    for (size_t i = 0; i < m; ++i) {
+        const ks_arc& a = arcs[i];
+        if (a.low > (uint64_t)INT64_MAX || a.cap > (uint64_t)INT64_MAX)
+            return c->fail(KS_E_RANGE, "arc bound exceeds int64");
+        int rc = upsert_arc(c, a.src, a.dst, (int64_t)a.low, (int64_t)a.cap, a.cost, a.type);
+        if (rc) return rc;
+    }
+    return KS_OK;
+}
+
+int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
+    if (!c) return KS_E_INVALID;
+    if (k && !d) return c->fail(KS_E_INVALID, "null delta array");
+    c->dirty = true;
+    c->have_solution = false;
+    for (size_t i = 0; i < k; ++i) {
+        const ks_delta& x = d[i];
+        int rc = KS_OK;
+        switch (x.kind) {
+            case KS_ADD_NODE:
+                rc = add_node(c, x.id, x.excess, x.type);
+                break;
+            case KS_REMOVE_NODE:
+                rc = remove_node(c, x.id);
+                break;
+            case KS_ADD_ARC:
+                if (x.low > (uint64_t)INT64_MAX || x.cap > (uint64_t)INT64_MAX) {
+                    rc = c->fail(KS_E_RANGE, "arc bound exceeds int64");
+                    break;
+                }
+                rc = upsert_arc(c, x.src, x.dst, (int64_t)x.low, (int64_t)x.cap, x.cost, x.type);
+                break;
+            case KS_UPDATE_ARC: {
+                if (x.low == 0 && x.cap == 0) {  // DeleteArc / ChangeArc(0,0): no capacity left
+                    auto it = c->arc_of.find(arc_key(x.src, x.dst));
+                    if (it != c->arc_of.end()) kill_arc(c, it->second);
+                    else if (!node_alive(c, x.src) || !node_alive(c, x.dst))
+                        rc = c->fail(KS_E_INVALID, "update of arc with a missing endpoint");
+                    break;
+                }
+                if (x.low > (uint64_t)INT64_MAX || x.cap > (uint64_t)INT64_MAX) {
+                    rc = c->fail(KS_E_RANGE, "arc bound exceeds int64");
+                    break;
+                }
+                rc = upsert_arc(c, x.src, x.dst, (int64_t)x.low, (int64_t)x.cap, x.cost, x.type);
+                break;
+            }
+            case KS_SET_EXCESS:
+                if (!node_alive(c, x.id)) rc = c->fail(KS_E_INVALID, "excess of missing node " + std::to_string(x.id));
+                else c->nodes[x.id].excess = x.excess;
+                break;
+            default:
+                rc = c->fail(KS_E_INVALID, "unknown delta kind " + std::to_string(x.kind));
+        }
+        if (rc) return rc;
+    }
+    return KS_OK;
+}
+
+int ks_solve(ks_ctx* c, ks_result* out) {
+    if (!c) return KS_E_INVALID;
+    ks_result r;
+    std::memset(&r, 0, sizeof(r));
+    c->have_solution = false;
+    c->flows_fresh = false;
+    int rc = KS_OK;
+    if (c->dirty) rc = upload(c);
+    if (rc == KS_OK) rc = c->eng.solve(r, c->err);
+    if (rc == KS_OK) {
+        int64_t pos = 0;
+        for (int64_t v : c->c_supply)
+            if (v > 0) pos += v;
+        r.flow_value = pos;
+        c->have_solution = true;
+    }
+    r.status = rc;
+    if (out) *out = r;
+    return rc;
+}
+
+int ks_get_flows(ks_ctx* c, ks_flow* out, size_t cap, size_t* count) {
+    if (!c || !count) return KS_E_INVALID;
+    int rc = fetch_flows(c);
+    if (rc) return rc;
+    size_t k = 0;
+    for (size_t i = 0; i < c->flows.size(); ++i)
+        if (c->flows[i] > 0) {
+            if (out && k < cap) {
+                const ArcRec& a = c->arcs[c->up_arc[i]];
+                out[k] = ks_flow{a.src, a.dst, c->flows[i]};
+            }
+            ++k;
+        }
+    *count = k;
+    return KS_OK;
+}
+
+int ks_get_task_mapping(ks_ctx* c, uint64_t* task, uint64_t* pu, size_t cap, size_t* count) {
+    if (!c || !count) return KS_E_INVALID;
+    int rc = fetch_flows(c);
+    if (rc) return rc;
+    std::vector<uint64_t> t, p;
+    task_mapping(c, t, p);
+    *count = t.size();
+    if (task && pu) {
+        const size_t k = std::min(cap, t.size());
+        std::copy(t.begin(), t.begin() + k, task);
+        std::copy(p.begin(), p.begin() + k, pu);
+    }
+    return KS_OK;
+}
+
+int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* count) {
+    if (!c || !count) return KS_E_INVALID;
+    int rc = fetch_flows(c);
+    if (rc) return rc;
+    std::vector<uint64_t> t, p;
+    task_mapping(c, t, p);
+    std::vector<uint64_t> dense;
+    size_t ti = 0;
+    for (int64_t v = 0; v < c->n_slots; ++v) {
+        const NodeRec& r = c->nodes[v + 1];
+        if (!r.alive || r.type != KS_NODE_TASK) continue;
+        uint64_t val = 0;
+        if (ti < t.size() && t[ti] == (uint64_t)v + 1) val = p[ti++];
+        dense.push_back(val);
+    }
+    *count = dense.size();
+    if (dev_out && cap) {
+        const size_t k = std::min(cap, dense.size());
+        return c->eng.copy_to_device(dev_out, dense.data(), k * sizeof(uint64_t), c->err);
+    }
+    return KS_OK;
+}
+
+}  // extern "C"

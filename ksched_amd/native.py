@@ -1,0 +1,194 @@
+"""ctypes binding of libksmcmf.so (include/ksmcmf.h).
+
+The product path: every call goes to the in-tree HIP library. There is no CPU
+fallback — if the library or a HIP device is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _build
+
+KS_OK, KS_E_INVALID, KS_E_INFEASIBLE, KS_E_DEVICE, KS_E_VERIFY, KS_E_RANGE = 0, -1, -2, -3, -4, -5
+KS_ADD_NODE, KS_REMOVE_NODE, KS_ADD_ARC, KS_UPDATE_ARC, KS_SET_EXCESS = 0, 1, 2, 3, 4
+
+EXPORTED_SYMBOLS = (
+    "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
+    "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device",
+)
+
+NODE_DT = np.dtype({"names": ["id", "excess", "type", "_pad"],
+                    "formats": ["<u8", "<i8", "<i4", "<i4"], "offsets": [0, 8, 16, 20], "itemsize": 24})
+ARC_DT = np.dtype({"names": ["src", "dst", "low", "cap", "cost", "type", "_pad"],
+                   "formats": ["<u8", "<u8", "<u8", "<u8", "<i8", "<i4", "<i4"],
+                   "offsets": [0, 8, 16, 24, 32, 40, 44], "itemsize": 48})
+DELTA_DT = np.dtype({"names": ["kind", "type", "id", "src", "dst", "low", "cap", "cost", "old_cost", "excess"],
+                     "formats": ["<i4", "<i4", "<u8", "<u8", "<u8", "<u8", "<u8", "<i8", "<i8", "<i8"],
+                     "offsets": [0, 4, 8, 16, 24, 32, 40, 48, 56, 64], "itemsize": 72})
+FLOW_DT = np.dtype({"names": ["src", "dst", "flow"], "formats": ["<u8", "<u8", "<i8"],
+                    "offsets": [0, 8, 16], "itemsize": 24})
+
+
+class KsOpts(C.Structure):
+    _fields_ = [("alpha", C.c_int32), ("verify", C.c_int32), ("auto_sink", C.c_int32),
+                ("sweeps_per_batch", C.c_int32), ("gu_interval", C.c_int32), ("reserved", C.c_int32 * 11)]
+
+
+class KsResult(C.Structure):
+    _fields_ = [("total_cost", C.c_int64), ("flow_value", C.c_int64), ("status", C.c_int32),
+                ("phases", C.c_int32), ("sweeps", C.c_uint64), ("arc_scans", C.c_uint64),
+                ("node_visits", C.c_uint64), ("pushes", C.c_uint64), ("relabels", C.c_uint64),
+                ("global_updates", C.c_uint64), ("gu_iterations", C.c_uint64), ("gu_arc_scans", C.c_uint64),
+                ("ms_phase", C.c_double * 6), ("n_nodes", C.c_int64), ("n_arcs", C.c_int64),
+                ("sweep_launches", C.c_uint64), ("ms_sweep_kernels", C.c_double),
+                ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ms_phase"}
+        names = ("build", "saturate", "sweeps", "global_update", "verify", "total")
+        d["ms"] = dict(zip(names, list(self.ms_phase)))
+        return d
+
+
+class KsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ksmcmf error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True):
+    """Load the in-tree library (building it with hipcc if absent and allowed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
+        _build.build()
+    L = C.CDLL(path)
+    P, V = C.POINTER, C.c_void_p
+    L.ks_abi_version.restype = C.c_int
+    L.ks_default_opts.argtypes = [P(KsOpts)]
+    L.ks_create.argtypes = [C.c_int, P(KsOpts)]
+    L.ks_create.restype = V
+    L.ks_destroy.argtypes = [V]
+    L.ks_last_error.argtypes = [V]
+    L.ks_last_error.restype = C.c_char_p
+    L.ks_load_graph.argtypes = [V, V, C.c_size_t, V, C.c_size_t]
+    L.ks_apply_deltas.argtypes = [V, V, C.c_size_t]
+    L.ks_solve.argtypes = [V, P(KsResult)]
+    L.ks_get_flows.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
+    L.ks_get_task_mapping.argtypes = [V, V, V, C.c_size_t, P(C.c_size_t)]
+    L.ks_get_task_pu_device.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
+    _LIB = L
+    return L
+
+
+def default_opts(**kw) -> KsOpts:
+    o = KsOpts()
+    load().ks_default_opts(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+@dataclass
+class SolveResult:
+    cost: int
+    flow: int
+    raw: dict
+
+
+class Context:
+    """One solver context on one HIP device (ks_create … ks_destroy)."""
+
+    def __init__(self, device: int = 0, **opts):
+        self._L = load()
+        self.opts = default_opts(**opts)
+        h = self._L.ks_create(device, C.byref(self.opts))
+        if not h:
+            raise KsError(KS_E_DEVICE, f"ks_create failed: no usable HIP device {device}")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ks_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != KS_OK:
+            raise KsError(rc, self._L.ks_last_error(self._h).decode(errors="replace"))
+
+    # -- graph upload -------------------------------------------------------
+    def load_arrays(self, nodes: np.ndarray, arcs: np.ndarray):
+        nodes = np.ascontiguousarray(nodes, NODE_DT)
+        arcs = np.ascontiguousarray(arcs, ARC_DT)
+        self._check(self._L.ks_load_graph(self._h, nodes.ctypes.data, nodes.shape[0],
+                                          arcs.ctypes.data, arcs.shape[0]))
+
+    def load_graph(self, g):
+        """Upload a ksched_amd.gen.Graph (1-based ids, all nodes alive)."""
+        nodes = np.zeros(g.n, NODE_DT)
+        nodes["id"] = np.arange(1, g.n + 1, dtype=np.uint64)
+        nodes["excess"] = g.supply
+        nodes["type"] = g.ntype
+        arcs = np.zeros(g.m, ARC_DT)
+        arcs["src"], arcs["dst"] = g.src, g.dst
+        arcs["low"], arcs["cap"], arcs["cost"] = g.low, g.cap, g.cost
+        arcs["type"] = g.arc_types()
+        self.load_arrays(nodes, arcs)
+
+    def apply_deltas(self, deltas: np.ndarray):
+        deltas = np.ascontiguousarray(deltas, DELTA_DT)
+        self._check(self._L.ks_apply_deltas(self._h, deltas.ctypes.data, deltas.shape[0]))
+
+    # -- solve & results ----------------------------------------------------
+    def solve(self) -> SolveResult:
+        r = KsResult()
+        rc = self._L.ks_solve(self._h, C.byref(r))
+        self._check(rc)
+        return SolveResult(r.total_cost, r.flow_value, r.as_dict())
+
+    def flows(self) -> np.ndarray:
+        cnt = C.c_size_t()
+        self._check(self._L.ks_get_flows(self._h, None, 0, C.byref(cnt)))
+        out = np.zeros(cnt.value, FLOW_DT)
+        self._check(self._L.ks_get_flows(self._h, out.ctypes.data, cnt.value, C.byref(cnt)))
+        return out
+
+    def task_mapping(self) -> dict[int, int]:
+        cnt = C.c_size_t()
+        self._check(self._L.ks_get_task_mapping(self._h, None, None, 0, C.byref(cnt)))
+        t = np.zeros(cnt.value, np.uint64)
+        p = np.zeros(cnt.value, np.uint64)
+        self._check(self._L.ks_get_task_mapping(self._h, t.ctypes.data, p.ctypes.data, cnt.value, C.byref(cnt)))
+        return dict(zip(t.tolist(), p.tolist()))
+
+    def task_pu_device(self, dev_ptr: int, cap: int) -> int:
+        cnt = C.c_size_t()
+        self._check(self._L.ks_get_task_pu_device(self._h, C.c_void_p(dev_ptr), cap, C.byref(cnt)))
+        return cnt.value

@@ -1,0 +1,203 @@
+"""GPU parity: the HIP solver (through the C-ABI) against the CPU oracle and the
+committed goldens. Bit-exact total cost and flow value; flows verified for
+capacity and conservation; task mappings validated (SURVEY §7 hard part 5)."""
+import numpy as np
+import pytest
+
+from conftest import load_goldens, load_known_answers
+from graphs import graph_from_lists, random_graphs
+from ksched_amd import gen, native
+from oracle import ko
+
+pytestmark = pytest.mark.gpu
+
+
+def flows_by_arc(ctx, g):
+    """Per-input-arc flow vector from the f lines."""
+    f = ctx.flows()
+    idx = {(int(s), int(d)): i for i, (s, d) in enumerate(zip(g.src.tolist(), g.dst.tolist()))}
+    out = np.zeros(g.m, np.int64)
+    for s, d, x in zip(f["src"].tolist(), f["dst"].tolist(), f["flow"].tolist()):
+        out[idx[(s, d)]] = x
+    return out
+
+
+def check_mapping(g, mapping):
+    pu_cap = {}
+    for s, d, c in zip(g.src.tolist(), g.dst.tolist(), g.cap.tolist()):
+        if g.ntype[s - 1] == 2 and g.ntype[d - 1] == 3:
+            pu_cap[s] = c
+    load = {}
+    for t, p in mapping.items():
+        assert g.ntype[t - 1] == 1, "mapped node is not a task"
+        assert g.ntype[p - 1] == 2, "task mapped to a non-PU node"   # graph_manager.go:259-262
+        load[p] = load.get(p, 0) + 1
+    for p, k in load.items():
+        assert k <= pu_cap.get(p, k), "PU over capacity"
+
+
+def solve_and_check(ctx, g, cost, flow, check_flows=True):
+    ctx.load_graph(g)
+    r = ctx.solve()
+    assert r.cost == cost
+    assert r.flow == flow
+    if check_flows:
+        fl = flows_by_arc(ctx, g)
+        st, c2, _ = ko.verify(g, fl)
+        assert st == 0, "oracle verifier rejected the GPU flow"
+        assert c2 == cost
+    return r
+
+
+def test_config1_known_answer(ctx):
+    ka = load_known_answers()["config1"]
+    g = gen.trivial(*ka["params"])
+    assert (g.n, g.m) == (ka["n"], ka["m"])
+    solve_and_check(ctx, g, ka["cost"], ka["flow"])
+    mp = ctx.task_mapping()
+    assert len(mp) == 100          # every pod placed through the cluster EC (cost 2 < 5)
+    check_mapping(g, mp)
+
+
+def test_multi_schedule_round1(ctx):
+    r1 = load_known_answers()["multi_schedule_iteration"]["round1_graph"]
+    g = graph_from_lists(r1["nodes"], r1["arcs"])
+    solve_and_check(ctx, g, r1["cost"], r1["flow"])
+    mp = ctx.task_mapping()
+    assert len(mp) == 2
+    check_mapping(g, mp)
+
+
+@pytest.mark.parametrize("e", [e for e in load_goldens() if e["m"] <= 60000],
+                         ids=lambda e: f"{e['family']}-{'x'.join(map(str, e['params']))}-s{e['seed']}")
+def test_goldens(ctx, e):
+    g = gen.trivial(*e["params"]) if e["family"] == "trivial" else gen.quincy(*e["params"], e["seed"])
+    solve_and_check(ctx, g, e["cost"], e["flow"])
+    check_mapping(g, ctx.task_mapping())
+
+
+def test_reference_bfs_accepts_gpu_flow(ctx):
+    """The reference's own decomposition (solver.go:183-269) over the GPU f lines."""
+    g = gen.quincy(3000, 300, 12, 30, 10)
+    ctx.load_graph(g)
+    r = ctx.solve()
+    fl = flows_by_arc(ctx, g)
+    ref_map = ko.bfs_mapping(g, fl, r.cost)
+    mp = ctx.task_mapping()
+    assert len(ref_map) == len(mp)
+    check_mapping(g, ref_map)
+
+
+def test_config3_full_size(ctx):
+    T, M, R, J, seed = gen.CONFIGS["config3"]
+    g = gen.quincy(T, M, R, J, seed)
+    gold = [e for e in load_goldens() if e["params"] == [T, M, R, J] and e["seed"] == seed]
+    if gold:
+        cost = gold[0]["cost"]
+    else:
+        st, cost, fv, _ = ko.cost_scaling(g)
+        assert st == 0
+    solve_and_check(ctx, g, cost, T)
+    check_mapping(g, ctx.task_mapping())
+
+
+# ----------------------------------------------------------------- edge cases ---
+def test_empty_graph(ctx):
+    ctx.load_arrays(np.zeros(0, native.NODE_DT), np.zeros(0, native.ARC_DT))
+    r = ctx.solve()
+    assert (r.cost, r.flow) == (0, 0)
+
+
+def test_isolated_nodes_no_arcs(ctx):
+    nodes = [(1, 0, 3), (2, 0, 0), (5, 0, 1)]
+    g = graph_from_lists(nodes, np.zeros((0, 5), np.int64))
+    ctx.load_graph(g)
+    r = ctx.solve()
+    assert (r.cost, r.flow) == (0, 0)
+
+
+def test_infeasible_reports_error(ctx):
+    # 3 tasks, one PU slot, no unscheduled escape → supply cannot reach the sink
+    nodes = [(1, -3, 3), (2, 0, 2), (3, 1, 1), (4, 1, 1), (5, 1, 1)]
+    arcs = [(2, 1, 0, 1, 0), (3, 2, 0, 1, 1), (4, 2, 0, 1, 1), (5, 2, 0, 1, 1)]
+    g = graph_from_lists(nodes, arcs)
+    ctx.load_graph(g)
+    with pytest.raises(native.KsError) as ei:
+        ctx.solve()
+    assert ei.value.code == native.KS_E_INFEASIBLE
+
+
+def test_lower_bound_running_arc(ctx):
+    # pinned task: running arc low=1 cap=1 to a PU (graph_manager.go:675-720)
+    nodes = [(1, -2, 3), (2, 0, 2), (3, 0, 2), (4, 1, 1), (5, 1, 1), (6, 0, 0)]
+    arcs = [(2, 1, 0, 5, 0), (3, 1, 0, 5, 0), (4, 3, 1, 1, 7), (5, 2, 0, 1, 3), (5, 6, 0, 1, 5), (6, 1, 0, 2, 0)]
+    g = graph_from_lists(nodes, arcs)
+    st, c, fv, _, _ = ko.ssp(g)
+    assert st == 0
+    solve_and_check(ctx, g, c, fv)
+    assert ctx.task_mapping() == {4: 3, 5: 2}
+
+
+def test_random_graphs_vs_oracle(ctx):
+    for trial, g in random_graphs(12345, 40):
+        st, c, fv, _, _ = ko.ssp(g)
+        ctx.load_graph(g)
+        if st == 0:
+            solve_and_check(ctx, g, c, fv)
+        else:
+            with pytest.raises(native.KsError) as ei:
+                ctx.solve()
+            assert ei.value.code == native.KS_E_INFEASIBLE
+
+
+def test_deltas_match_full_reload(ctx):
+    """Incremental protocol (ExportIncremental: n / r / a / x lines) vs a full export."""
+    g = gen.quincy(1000, 100, 5, 10, 4)
+    ctx.load_graph(g)
+    r0 = ctx.solve()
+    # complete the first 50 tasks ("r id"), add 30 new tasks with 5 arcs each,
+    # raise the unscheduled cost of 100 waiting tasks ("x" lines)
+    R, M = 5, 100
+    TASK0 = 3 + R + 2 * M + 10
+    U0 = 3 + R + 2 * M
+    d = []
+    removed = list(range(TASK0, TASK0 + 50))
+    for t in removed:
+        d.append(dict(kind=native.KS_REMOVE_NODE, id=t))
+    new_ids = removed[:30]     # FIFO id reuse (graph.go:169-182)
+    rng = np.random.default_rng(7)
+    new_arcs = []
+    for t in new_ids:
+        d.append(dict(kind=native.KS_ADD_NODE, id=t, excess=1, type=1))
+        j = int(rng.integers(0, 10))
+        m1, m2 = (int(x) for x in rng.choice(M, 2, replace=False))
+        for dst, cost in ((U0 + j, 500), (2, 250), (3 + int(rng.integers(0, R)), 100),
+                          (3 + R + m1, 10), (3 + R + m2, 20)):
+            d.append(dict(kind=native.KS_ADD_ARC, src=t, dst=dst, low=0, cap=1, cost=cost))
+            new_arcs.append((t, dst, 0, 1, cost))
+    upd = {}
+    src, dst, cost = g.src.tolist(), g.dst.tolist(), g.cost.tolist()
+    for i in range(5 * 60, 5 * 160, 5):     # task→U arcs of 100 surviving tasks
+        d.append(dict(kind=native.KS_UPDATE_ARC, src=src[i], dst=dst[i], low=0, cap=1, cost=cost[i] + 10,
+                      old_cost=cost[i]))
+        upd[(src[i], dst[i])] = cost[i] + 10
+    arr = np.zeros(len(d), native.DELTA_DT)
+    for i, x in enumerate(d):
+        for k, v in x.items():
+            arr[i][k] = v
+    ctx.apply_deltas(arr)
+    r1 = ctx.solve()
+    # equivalent full graph
+    keep = [i for i in range(g.m) if src[i] not in removed and dst[i] not in removed]
+    arcs = [(src[i], dst[i], int(g.low[i]), int(g.cap[i]), upd.get((src[i], dst[i]), cost[i])) for i in keep]
+    arcs += new_arcs
+    sup = g.supply.copy()
+    for t in removed[30:]:
+        sup[t - 1] = 0
+    sup[0] = -int(sup[1:].sum())          # auto-sink: the sink absorbs every other supply
+    nodes = [(i + 1, int(sup[i]), int(g.ntype[i])) for i in range(g.n)]
+    h = graph_from_lists(nodes, arcs)
+    st, c, fv, _, _ = ko.ssp(h)
+    assert st == 0
+    assert (r1.cost, r1.flow) == (c, fv)
+    assert r0.flow == 1000 and r1.flow == 980
