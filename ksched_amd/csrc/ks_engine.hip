@@ -35,6 +35,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -57,6 +59,7 @@ constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp (safe: DESIGN.md §3.3)
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
+constexpr long long kTraceMax = 1 << 16;  // sweeps recorded when KS_TRACE is set
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4 };
 
@@ -103,6 +106,7 @@ struct DG {
     long long* dist;
     Ctl* ctl;
     unsigned long long* ctr;
+    unsigned* trace;   // optional per-sweep [visits, relabels] (KS_TRACE diagnostics)
     int nmblocks;   // medium blocks = ceil(nmedium / WPB)
 };
 
@@ -618,14 +622,17 @@ __device__ void heavy_chunk(const DG& g, const HItem& it, const long long* __res
                 else np = px - (mn + eps);
                 c.relabel++;
             }
-            if (ex > 0) act = 1;
+            if (ex > 0) {
+                act = 1;
+                c.visit++;
+            }
             PN[x] = np;
             atom_exch_i(&g.harrive[h], 0);
         }
     }
 }
 
-__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos) {
+__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int tidx) {
     const int prev = pos ? g.ctl->active[pos - 1] : g.ctl->active_prev;
     if (!prev) return;
     const long long eps = g.ctl->eps;
@@ -651,6 +658,15 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos) {
         }
     }
     if (__any(act) && lane_id() == 0) g.ctl->active[pos] = 1;
+    if (g.trace && tidx >= 0) {
+        const long long v = wave_sum(c.visit), r = wave_sum(c.relabel);
+        if (lane_id() == 0 && (v | r)) {
+            const int cls = blockIdx.x < g.nhitems ? 3 : (blockIdx.x < g.nhitems + g.nmblocks ? 2 : -1);
+            atomicAdd(&g.trace[4 * tidx], (unsigned)v);
+            atomicAdd(&g.trace[4 * tidx + 1], (unsigned)r);
+            if (cls > 0) atomicAdd(&g.trace[4 * tidx + cls], (unsigned)v);
+        }
+    }
     flush_counters(g, c);
 }
 
@@ -896,6 +912,7 @@ struct EngineImpl {
     DBuf<int> hnchunks, harrive, hunsat;
     DBuf<long long> hmin, inbox, part, flows;
     DBuf<unsigned long long> ctr;
+    DBuf<unsigned> trace;
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;       // pinned host mirror
     long long* h_scr = nullptr; // pinned scratch: [0] eps, [1] constant 1
@@ -913,7 +930,7 @@ struct EngineImpl {
         rcap.release(); scost.release(); excess.release(); p0.release(); p1.release(); dist.release();
         cls.release(); hidx.release(); light.release(); medium.release(); heavy.release(); nsel.release();
         sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release(); hunsat.release();
-        hmin.release(); inbox.release(); part.release(); flows.release(); ctr.release(); ctl.release();
+        hmin.release(); inbox.release(); part.release(); flows.release(); ctr.release(); trace.release(); ctl.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
@@ -952,6 +969,7 @@ struct EngineImpl {
         g.dist = dist.p;
         g.ctl = ctl.p;
         g.ctr = ctr.p;
+        g.trace = trace.n ? trace.p : nullptr;
         g.nmblocks = (nmedium + WPB - 1) / WPB;
         return g;
     }
@@ -1090,6 +1108,17 @@ int Engine::solve(ks_result& res, std::string& err) {
     KS_CHECK(s.part.ensure(4096));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
+    const char* trace_path = std::getenv("KS_TRACE");
+    if (trace_path && *trace_path) {
+        KS_CHECK(s.trace.ensure(4 * kTraceMax));
+        KS_CHECK(hipMemsetAsync(s.trace.p, 0, 4 * kTraceMax * sizeof(unsigned), st));
+    }
+    struct PhaseRec {
+        long long eps;
+        uint64_t begin, end;
+        std::vector<uint64_t> gu_at;
+    };
+    std::vector<PhaseRec> ptrace;
 
     if (m) {
         hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
@@ -1237,6 +1266,7 @@ int Engine::solve(ks_result& res, std::string& err) {
         KS_CHECK(hipEventRecord(s.ev[2], st));
         hipLaunchKernelGGL(k_saturate, dim3(sgrid), dim3(BLK), 0, st, g);
         KS_CHECK(hipEventRecord(s.ev[3], st));
+        ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}});
         int rc = global_update();
         if (rc) return rc;
         KS_CHECK(hipEventRecord(s.ev[4], st));
@@ -1246,7 +1276,11 @@ int Engine::solve(ks_result& res, std::string& err) {
             KS_CHECK(hipMemsetAsync(s.ctl.p->active, 0, sizeof(int) * K, st));
             KS_CHECK(hipMemcpyAsync(&s.ctl.p->active_prev, one, sizeof(int), hipMemcpyHostToDevice, st));
             KS_CHECK(hipEventRecord(s.kev[2], st));
-            for (int k = 0; k < K; ++k) hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k);
+            for (int k = 0; k < K; ++k) {
+                const long long ti = (long long)sweep_launches + k;
+                hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k,
+                                   (g.trace && ti < kTraceMax) ? (int)ti : -1);
+            }
             KS_CHECK(hipEventRecord(s.kev[3], st));
             KS_CHECK(read_ctl());
             sweep_launches += K;
@@ -1261,6 +1295,7 @@ int Engine::solve(ks_result& res, std::string& err) {
             if (!s.h_ctl->active[K - 1]) break;
             since_gu += K;
             if (since_gu >= gu_interval) {
+                ptrace.back().gu_at.push_back(sweep_launches);
                 KS_CHECK(hipEventRecord(s.ev[6], st));
                 rc = global_update();
                 if (rc) return rc;
@@ -1284,6 +1319,7 @@ int Engine::solve(ks_result& res, std::string& err) {
         }
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
+        ptrace.back().end = sweep_launches;
         ms_sat += ev_ms(s.ev[2], s.ev[3]);
         ms_gu += ev_ms(s.ev[3], s.ev[4]);
         ms_sweep += ev_ms(s.ev[4], s.ev[5]);
@@ -1331,6 +1367,29 @@ int Engine::solve(ks_result& res, std::string& err) {
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
 
+    if (trace_path && *trace_path && s.trace.n) {
+        const uint64_t nt = std::min<uint64_t>(sweep_launches, kTraceMax);
+        std::vector<unsigned> ht(4 * nt);
+        if (nt) KS_CHECK(hipMemcpy(ht.data(), s.trace.p, 4 * nt * sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(trace_path, "a")) {
+            std::fprintf(f, "{\"n\": %lld, \"m\": %lld, \"phases\": [", (long long)n, (long long)m);
+            for (size_t i = 0; i < ptrace.size(); ++i) {
+                std::fprintf(f, "%s{\"eps\": %lld, \"begin\": %llu, \"end\": %llu, \"gu_at\": [", i ? ", " : "",
+                             ptrace[i].eps, (unsigned long long)ptrace[i].begin, (unsigned long long)ptrace[i].end);
+                for (size_t k = 0; k < ptrace[i].gu_at.size(); ++k)
+                    std::fprintf(f, "%s%llu", k ? ", " : "", (unsigned long long)ptrace[i].gu_at[k]);
+                std::fprintf(f, "]}");
+            }
+            std::fprintf(f, "], ");
+            const char* names[4] = {"visits", "relabels", "medium", "heavy"};
+            for (int k = 0; k < 4; ++k) {
+                std::fprintf(f, "%s\"%s\": [", k ? "], " : "", names[k]);
+                for (uint64_t i = 0; i < nt; ++i) std::fprintf(f, "%s%u", i ? ", " : "", ht[4 * i + k]);
+            }
+            std::fprintf(f, "]}\n");
+            std::fclose(f);
+        }
+    }
     res.total_cost = tot_cost;
     res.phases = phases;
     res.sweeps = sweeps;
