@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--alpha", type=int, default=0)
     ap.add_argument("--gu-interval", type=int, default=0)
-    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--price-refine", type=int, default=-1)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -58,8 +58,8 @@ def main():
         opts["alpha"] = args.alpha
     if args.gu_interval:
         opts["gu_interval"] = args.gu_interval
-    if args.batch:
-        opts["sweeps_per_batch"] = args.batch
+    if args.price_refine >= 0:
+        opts["price_refine"] = args.price_refine
     ctx = native.Context(local, **opts)
     ctx.load_graph(g)
 

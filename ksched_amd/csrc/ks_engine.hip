@@ -6,30 +6,46 @@
 //
 //   build      residual CSR from the device-resident input arcs: a stable radix
 //              sort of the 2m (tail, slot) keys (hipcub over rocPRIM), lower
-//              bounds transformed into node excess, nodes split by degree into
-//              light (thread per node), medium (wave per node) and heavy
-//              (1024-arc chunks, one workgroup per chunk) lists.
-//   phases     ε ← ε/α; saturate every residual arc with negative reduced cost;
-//              global price update; then synchronous push/relabel sweeps until
-//              no node holds positive excess, with periodic global updates.
-//   sweep      every node with positive excess discharges once per sweep
-//              against a price SNAPSHOT (prices are double-buffered: the sweep
-//              reads P[q] and writes P[q^1]); a node relabels only if it
-//              saturated all of its own admissible arcs, and its relabel amount
-//              also covers arcs that may gain residual capacity from concurrent
-//              pushes in the same sweep (reduced cost in (0, ε]) — this keeps
+//              bounds transformed into node excess. Nodes are classed by degree
+//              into lane GROUPS of 4/8/16/32/64 lanes per node (one residual arc
+//              per lane: a node costs one short dependent chain, not a serial
+//              arc loop) plus heavy hubs (1024-arc chunks, one workgroup per
+//              chunk). An ORDER array lists the nodes class by class, each class
+//              padded to 64 slots, so a 64-slot window is single-class.
+//   phases     ε ← ε/α: saturate every residual arc with negative reduced cost,
+//              then alternate a GLOBAL PRICE UPDATE (Bellman-Ford from the
+//              deficits) with a short burst of push/relabel SWEEPS until no node
+//              holds excess. Once ε is below a small fraction of a cost unit the
+//              flow is tested by PRICE REFINEMENT at ε = 1 (Bellman-Ford on the
+//              difference constraints of 1-optimality); success proves the flow
+//              optimal and ends the solve early.
+//   frontier   sweeps and Bellman-Ford rounds only touch the ACTIVE frontier:
+//              one flag byte per order slot (three rotating buffers) plus
+//              per-hub flags. Producers store 1 (idempotent, no counters, no
+//              returning atomics); the consumer ballots 64 flags per wave,
+//              clears what it reads and hands active nodes to its lane groups.
+//              Dense passes (saturate, the first round of an update) map every
+//              group to one node statically instead.
+//   sweep      every frontier node discharges once against a price SNAPSHOT
+//              (double-buffered prices: read P[q], write P[q^1]); a node
+//              relabels only if it saturated all of its own admissible arcs, and
+//              the relabel also covers arcs that may gain residual capacity from
+//              concurrent pushes in the same sweep (reduced cost in (0, ε]) —
 //              ε-optimality without locks.
-//   heavy hubs pushes into a hub (cluster aggregator, sink: in-degree ~10^5)
-//              are wave-aggregated into a 16-way sharded inbox that the hub's
-//              first chunk drains; hub chunks claim excess with a CAS and the
-//              last-arriving chunk (RMW-atomic arrival counter) finalises the
-//              relabel.
-//   verify     on-device: conservation (all excess zero), capacity, and
-//              1-optimality of the final prices in scaled units (costs scaled by
-//              n+1, so 1-optimal ⇒ optimal); the total cost is reduced in int64.
+//   control    the host enqueues one CYCLE per round trip: [global-update init]
+//              [k Bellman-Ford rounds] [max] [apply] [g sweeps]; kernels read
+//              device-side flags and exit early once their stage is finished,
+//              so a cycle costs one host synchronisation.
+//   heavy hubs pushes into a hub (cluster aggregator, sink) are wave-aggregated
+//              into a 16-way sharded inbox; hub chunks claim excess with a CAS
+//              and the last-arriving chunk finalises the relabel. Bellman-Ford
+//              relaxations into a hub are min-reduced in LDS per workgroup.
+//   verify     on-device: conservation, capacity, and 1-optimality of the final
+//              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
+//              the total cost is reduced in int64.
 //
-// All in-kernel cross-workgroup communication uses device-scope RMW atomics;
-// everything else is handed over at kernel boundaries.
+// All in-kernel cross-workgroup communication uses device-scope RMW atomics or
+// idempotent flag stores; everything else is handed over at kernel boundaries.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -48,35 +64,47 @@ namespace {
 constexpr int BLK = 256;
 constexpr int WAVE = 64;
 constexpr int WPB = BLK / WAVE;
-constexpr int LIGHT_MAX = 32;      // degree ≤ 32: one thread per node
-constexpr int MEDIUM_MAX = 4096;   // degree ≤ 4096: one wave per node
+constexpr int NGC = 5;             // group classes: 4, 8, 16, 32, 64 lanes per node
+constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
 constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
 constexpr int PER_T = CHUNK / BLK;
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
-constexpr int MAXB = 64;           // max kernels per host batch
+constexpr int MAXB = 64;           // max sweeps per cycle
+constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
 constexpr int NCTR = 8;
 constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
-constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp (safe: DESIGN.md §3.3)
+constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
-constexpr long long kTraceMax = 1 << 16;  // sweeps recorded when KS_TRACE is set
+constexpr long long kTraceMax = 1 << 16;   // sweeps recorded when KS_TRACE is set
 
-enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4 };
+enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5 };
 
 struct Ctl {
     long long eps;
-    int active_prev;
+    long long gu_L;        // max finite distance of the current global update
     int infeasible;
-    int active[MAXB];
-    int gu_prev;
-    int pad0;
-    int gu_changed[MAXB];
+    int bf_done;           // Bellman-Ford frontier drained (update converged)
     int verify_bad;
-    int pad1;
+    int bf_count;          // Bellman-Ford rounds that did work (whole solve)
+    int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
+    int apply_act;         // the global-update apply seeded a non-empty frontier
+    int sweep_act[MAXB];   // sweep pos left a non-empty frontier
 };
 
 struct HItem {
     int node, hid, begin, end;
+};
+
+__host__ __device__ constexpr int class_lanes(int c) { return c < 4 ? (4 << c) : 64; }
+__host__ __device__ inline int degree_class(int d) {
+    return d <= 4 ? 0 : d <= 8 ? 1 : d <= 16 ? 2 : d <= 32 ? 3 : d <= HEAVY_MIN ? 4 : NGC;
+}
+
+// One frontier buffer: a flag byte per order slot, a flag per hub.
+struct Front {
+    unsigned char* flag;   // [n_pad]
+    int* hub;              // [nheavy]
 };
 
 struct DG {
@@ -89,12 +117,14 @@ struct DG {
     long long* excess;
     long long* p0;
     long long* p1;
+    long long* dist;
     const int* hidx;
     long long* inbox;
-    const int* light;
-    int nlight;
-    const int* medium;
-    int nmedium;
+    const int* order;      // [n_pad] nodes class by class, −1 padding
+    const int* fidx;       // [n] node → order slot (−1 for hubs)
+    int n_pad;
+    int wbeg[NGC + 1];     // windows (one per wave) of class c: [wbeg[c], wbeg[c+1])
+    int obeg[NGC + 1];     // first order slot of class c
     const HItem* hitems;
     int nhitems;
     int nheavy;
@@ -103,11 +133,11 @@ struct DG {
     int* harrive;
     long long* hmin;
     int* hunsat;
-    long long* dist;
+    Front sf[3];   // sweep frontiers
+    Front bf[3];   // Bellman-Ford frontiers
     Ctl* ctl;
     unsigned long long* ctr;
-    unsigned* trace;   // optional per-sweep [visits, relabels] (KS_TRACE diagnostics)
-    int nmblocks;   // medium blocks = ceil(nmedium / WPB)
+    unsigned* trace;   // optional per-sweep [visits, relabels, groups, heavy] (KS_TRACE)
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -125,6 +155,12 @@ __device__ __forceinline__ int atom_exch_i(int* p, int v) {
 }
 __device__ __forceinline__ long long atom_min_ret(long long* p, long long v) {
     return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void atom_min(long long* p, long long v) {
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ long long atom_load(long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -153,10 +189,41 @@ __device__ __forceinline__ long long wave_incl_scan(long long x, int lane) {
     }
     return x;
 }
+// Lane-group (G lanes, aligned) collectives.
+template <int G>
+__device__ __forceinline__ long long g_incl_scan(long long x) {
+    const int l = lane_id() & (G - 1);
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+        long long y = __shfl_up(x, o, G);
+        if (l >= o) x += y;
+    }
+    return x;
+}
+template <int G>
+__device__ __forceinline__ long long g_min(long long x) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) x = min(x, (long long)__shfl_xor(x, o, G));
+    return x;
+}
+template <int G>
+__device__ __forceinline__ long long g_sum(long long x) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, G);
+    return x;
+}
 __device__ __forceinline__ long long floordiv(long long a, long long b) {  // b > 0
     long long q = a / b;
     if ((a % b) != 0 && a < 0) --q;
     return q;
+}
+
+// Mark node w active in frontier f (idempotent plain stores).
+__device__ __forceinline__ void mark(const DG& g, const Front& f, int w, int& out) {
+    const int h = g.hidx[w];
+    if (h >= 0) f.hub[h] = 1;
+    else f.flag[g.fidx[w]] = 1;
+    out = 1;
 }
 
 // Per-lane pending hub push: wave-aggregated into the hub's sharded inbox.
@@ -165,11 +232,40 @@ struct Pend {
     long long val;
 };
 
-__device__ __forceinline__ void push_excess(const DG& g, int w, long long d, Pend& pd) {
+struct Cnt {
+    long long scan = 0, visit = 0, push = 0, relabel = 0;
+};
+
+__device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
+    const long long s = wave_sum(c.scan), v = wave_sum(c.visit), p = wave_sum(c.push),
+                    r = wave_sum(c.relabel);
+    if (lane_id() == 0 && (s | v | p | r)) {
+        const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
+        unsigned long long* c0 = g.ctr + sh * NCTR;
+        if (s) atomicAdd(c0 + C_SCAN, (unsigned long long)s);
+        if (v) atomicAdd(c0 + C_VISIT, (unsigned long long)v);
+        if (p) atomicAdd(c0 + C_PUSH, (unsigned long long)p);
+        if (r) atomicAdd(c0 + C_RELABEL, (unsigned long long)r);
+    }
+}
+
+// Push d units of excess into node w (fire-and-forget atomics) and mark w in
+// the next frontier (nf may be null: the saturate pass tracks nothing).
+__device__ __forceinline__ void push_excess(const DG& g, const Front* nf, int w, long long d, Pend& pd, int& out) {
     const int h = g.hidx[w];
     if (h < 0) {
         atom_add(&g.excess[w], d);
-    } else if (pd.key == h) {
+        if (nf) {
+            nf->flag[g.fidx[w]] = 1;
+            out = 1;
+        }
+        return;
+    }
+    if (nf) {
+        nf->hub[h] = 1;
+        out = 1;
+    }
+    if (pd.key == h) {
         pd.val += d;
     } else if (pd.key < 0) {
         pd.key = h;
@@ -190,23 +286,6 @@ __device__ __forceinline__ void flush_pending(const DG& g, Pend& pd) {
         const long long s = wave_sum(pd.key == k ? pd.val : 0);
         if (lane == leader) atom_add(&g.inbox[k * SHARDS + (blockIdx.x & (SHARDS - 1))], s);
         if (pd.key == k) pd.key = -1;
-    }
-}
-
-struct Cnt {
-    long long scan = 0, visit = 0, push = 0, relabel = 0;
-};
-
-__device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
-    const long long s = wave_sum(c.scan), v = wave_sum(c.visit), p = wave_sum(c.push),
-                    r = wave_sum(c.relabel);
-    if (lane_id() == 0 && (s | v | p | r)) {
-        const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
-        unsigned long long* c0 = g.ctr + sh * NCTR;
-        if (s) atomicAdd(c0 + C_SCAN, (unsigned long long)s);
-        if (v) atomicAdd(c0 + C_VISIT, (unsigned long long)v);
-        if (p) atomicAdd(c0 + C_PUSH, (unsigned long long)p);
-        if (r) atomicAdd(c0 + C_RELABEL, (unsigned long long)r);
     }
 }
 
@@ -259,6 +338,59 @@ __device__ __forceinline__ long long block_excl_scan(long long x, long long* sh,
     return off + incl - x;
 }
 
+// --------------------------------------------------- frontier traversal ---
+// A wave owns one WINDOW of class C: win_batches(C) batches of 64/G order slots.
+// It ballots the window's flags (clearing what it reads; dense passes take every
+// real node), then hands the active nodes to its G-lane groups one batch at a
+// time. The loop trip count is wave-uniform, so CALL may use wave collectives.
+__host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
+__host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
+
+#define KS_WINDOW(C, ARGS, W, ...)                                                   \
+    {                                                                                \
+        constexpr int G_ = class_lanes(C);                                           \
+        constexpr int PER_ = 64 / G_;                                                \
+        constexpr int WS_ = win_slots(C);                                            \
+        const int base_ = g.obeg[C] + ((W) - g.wbeg[C]) * WS_;                       \
+        const int ln_ = lane_id();                                                   \
+        bool on_ = false;                                                            \
+        if (ln_ < WS_) {                                                             \
+            if ((ARGS).dense) {                                                      \
+                on_ = g.order[base_ + ln_] >= 0;                                     \
+            } else {                                                                 \
+                on_ = (ARGS).flags[base_ + ln_] != 0;                                \
+                if (on_) (ARGS).flags[base_ + ln_] = 0;                              \
+            }                                                                        \
+        }                                                                            \
+        unsigned long long mask_ = __ballot(on_);                                    \
+        const int k_ = ln_ / G_;                                                     \
+        while (mask_) {                                                              \
+            unsigned long long mm_ = mask_;                                          \
+            for (int j_ = 0; j_ < k_; ++j_) mm_ &= mm_ - 1;                          \
+            const int v = mm_ ? g.order[base_ + __ffsll((long long)mm_) - 1] : -1;   \
+            __VA_ARGS__;                                                             \
+            for (int j_ = 0; j_ < PER_; ++j_) mask_ &= mask_ - 1;                    \
+        }                                                                            \
+    }
+// Dispatch on the (wave-uniform) class of window IDX.
+#define KS_BY_CLASS(IDX, ARGS, CALLT)                                                \
+    {                                                                                \
+        const int i_ = (IDX);                                                        \
+        if (i_ < g.wbeg[1]) KS_WINDOW(0, ARGS, i_, CALLT(0))                         \
+        else if (i_ < g.wbeg[2]) KS_WINDOW(1, ARGS, i_, CALLT(1))                    \
+        else if (i_ < g.wbeg[3]) KS_WINDOW(2, ARGS, i_, CALLT(2))                    \
+        else if (i_ < g.wbeg[4]) KS_WINDOW(3, ARGS, i_, CALLT(3))                    \
+        else if (i_ < g.wbeg[5]) KS_WINDOW(4, ARGS, i_, CALLT(4))                    \
+    }
+struct Scan {
+    unsigned char* flags;   // frontier flags to consume (sparse pass)
+    int dense;              // 1: every node, flags ignored
+};
+
+__device__ __forceinline__ int wave_index_in_grid(int first_block) {
+    return ((int)blockIdx.x - first_block) * WPB + ((int)threadIdx.x >> 6);
+}
+
 // ===================================================================== build ===
 __global__ void k_make_keys(int m, const int* __restrict__ src, const int* __restrict__ dst,
                             unsigned* __restrict__ keys, int* __restrict__ vals) {
@@ -305,14 +437,14 @@ __global__ void k_first(int n, long long m2, const unsigned* __restrict__ keys, 
 
 __global__ void k_node_init(int n, const long long* __restrict__ supply, const int* __restrict__ first,
                             long long* __restrict__ excess, long long* __restrict__ p0, long long* __restrict__ p1,
-                            unsigned char* __restrict__ cls, int* __restrict__ hidx) {
+                            unsigned char* __restrict__ cls, int* __restrict__ hidx, int* __restrict__ fidx) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
         excess[v] = supply[v];
         p0[v] = 0;
         p1[v] = 0;
-        const int d = first[v + 1] - first[v];
-        cls[v] = d <= LIGHT_MAX ? 0 : (d <= MEDIUM_MAX ? 1 : 2);
+        cls[v] = (unsigned char)degree_class(first[v + 1] - first[v]);
         hidx[v] = -1;
+        fidx[v] = -1;
     }
 }
 
@@ -332,6 +464,16 @@ __global__ void k_set_hidx(int nheavy, const int* __restrict__ hnode, int* __res
     if (h < nheavy) hidx[hnode[h]] = h;
 }
 
+// order[obeg + i] = list[i], fidx[list[i]] = obeg + i (one class).
+__global__ void k_make_order(int cnt, int obeg, const int* __restrict__ list, int* __restrict__ order,
+                             int* __restrict__ fidx) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < cnt; i += (long long)gridDim.x * BLK) {
+        const int v = list[i];
+        order[obeg + i] = v;
+        fidx[v] = obeg + (int)i;
+    }
+}
+
 struct ClassIs {
     const unsigned char* cls;
     unsigned char c;
@@ -340,15 +482,49 @@ struct ClassIs {
 
 // ================================================= saturate (phase start) ===
 // Push the full residual capacity of every arc with negative reduced cost
-// (Goldberg's refine start); reads the authoritative price buffer p0.
+// (Goldberg's refine start) over the whole graph; reads the authoritative p0.
+template <int G>
+__device__ __forceinline__ void sat_group(const DG& g, int v, Pend& pd, int& out, Cnt& c) {
+    const long long* P = g.p0;
+    const int lig = lane_id() & (G - 1);
+    int b0 = 0, en = 0;
+    long long pv = 0;
+    if (v >= 0) {
+        b0 = g.first[v];
+        en = g.first[v + 1];
+        pv = P[v];
+    }
+    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;   // G == 64: one node per wave
+    long long tot = 0;
+    for (int it = 0; it < iters; ++it) {
+        const int a = b0 + it * G + lig;
+        if (a < en) {
+            const long long r = g.rcap[a];
+            if (r > 0) {
+                const int w = g.head[a];
+                if (g.cost[a] + pv - P[w] < 0) {
+                    g.rcap[a] = 0;
+                    g.rcap[g.rev[a]] += r;
+                    push_excess(g, nullptr, w, r, pd, out);
+                    tot += r;
+                    c.push++;
+                }
+            }
+        }
+        flush_pending(g, pd);
+    }
+    tot = g_sum<G>(tot);
+    if (v >= 0 && lig == 0 && tot) atom_add(&g.excess[v], -tot);
+}
+
 __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
     const long long* P = g.p0;
     Pend pd{-1, 0};
     Cnt c;
-    int b = blockIdx.x;
-    if (b < g.nhitems) {
+    int out = 0;
+    if ((int)blockIdx.x < g.nhitems) {
         __shared__ long long sh[WPB];
-        const HItem it = g.hitems[b];
+        const HItem it = g.hitems[blockIdx.x];
         const long long px = P[it.node];
         long long tot = 0;
         for (int k = 0; k < PER_T; ++k) {
@@ -360,7 +536,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
                     if (g.cost[a] + px - P[w] < 0) {
                         g.rcap[a] = 0;
                         g.rcap[g.rev[a]] += r;
-                        push_excess(g, w, r, pd);
+                        push_excess(g, nullptr, w, r, pd, out);
                         tot += r;
                         c.push++;
                     }
@@ -373,120 +549,36 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
         flush_counters(g, c);
         return;
     }
-    b -= g.nhitems;
-    if (b < g.nmblocks) {
-        const int wi = b * WPB + (threadIdx.x >> 6);
-        const int lane = lane_id();
-        if (wi < g.nmedium) {
-            const int v = g.medium[wi];
-            const long long pv = P[v];
-            const int e = g.first[v + 1];
-            long long tot = 0;
-            for (int a = g.first[v] + lane; a < e; a += WAVE) {
-                const long long r = g.rcap[a];
-                if (r > 0) {
-                    const int w = g.head[a];
-                    if (g.cost[a] + pv - P[w] < 0) {
-                        g.rcap[a] = 0;
-                        g.rcap[g.rev[a]] += r;
-                        push_excess(g, w, r, pd);
-                        tot += r;
-                        c.push++;
-                    }
-                }
-            }
-            tot = wave_sum(tot);
-            if (lane == 0 && tot) atom_add(&g.excess[v], -tot);
-        }
-        flush_pending(g, pd);
-        flush_counters(g, c);
-        return;
-    }
-    b -= g.nmblocks;
-    const int i = b * BLK + threadIdx.x;
-    if (i < g.nlight) {
-        const int v = g.light[i];
-        const long long pv = P[v];
-        const int e = g.first[v + 1];
-        long long tot = 0;
-        for (int a = g.first[v]; a < e; ++a) {
-            const long long r = g.rcap[a];
-            if (r > 0) {
-                const int w = g.head[a];
-                if (g.cost[a] + pv - P[w] < 0) {
-                    g.rcap[a] = 0;
-                    g.rcap[g.rev[a]] += r;
-                    push_excess(g, w, r, pd);
-                    tot += r;
-                    c.push++;
-                }
-            }
-        }
-        if (tot) atom_add(&g.excess[v], -tot);
-    }
+    const Scan sc{nullptr, 1};
+#define KS_SAT_CALL(C) sat_group<G_>(g, v, pd, out, c)
+    KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SAT_CALL)
+#undef KS_SAT_CALL
     flush_pending(g, pd);
     flush_counters(g, c);
 }
 
-__global__ void k_drain_all(DG g) {
-    const int h = blockIdx.x * BLK + threadIdx.x;
-    if (h < g.nheavy) drain_inbox(g, h, g.hnode[h]);
-}
-
 // =================================================== push/relabel sweep ===
-__device__ __forceinline__ void light_discharge(const DG& g, int v, const long long* __restrict__ P,
-                                                long long* __restrict__ PN, long long eps, Pend& pd, int& act,
-                                                Cnt& c) {
-    const long long e = g.excess[v];
-    if (e <= 0) return;
-    c.visit++;
-    const long long pv = P[v];
-    long long rem = e, minc = INF64;
-    const int b = g.first[v], en = g.first[v + 1];
-    int a = b;
-    for (; a < en; ++a) {
-        const long long r = g.rcap[a];
-        const int w = g.head[a];
-        const long long cr = g.cost[a] + pv - P[w];
-        if (cr < 0) {
-            if (r > 0) {
-                const long long d = r < rem ? r : rem;
-                g.rcap[a] = r - d;
-                g.rcap[g.rev[a]] += d;
-                push_excess(g, w, d, pd);
-                c.push++;
-                rem -= d;
-                if (rem == 0) { ++a; break; }
-            }
-        } else if (r > 0 || cr <= eps) {
-            minc = min(minc, cr);
-        }
+// One node per G-lane group, one residual arc per lane; admissible capacity is
+// distributed by an in-group prefix sum, the relabel minimum by a group min.
+template <int G>
+__device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v, const long long* __restrict__ P,
+                                            long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
+    const int lig = lane_id() & (G - 1);
+    long long e = 0;
+    if (v >= 0) e = g.excess[v];
+    const bool act = e > 0;
+    long long pv = 0;
+    int b0 = 0, en = 0;
+    if (act) {
+        pv = P[v];
+        b0 = g.first[v];
+        en = g.first[v + 1];
+        if (lig == 0) c.visit++;
     }
-    c.scan += a - b;
-    const long long pushed = e - rem;
-    if (pushed) atom_add(&g.excess[v], -pushed);
-    long long np = pv;
-    if (rem > 0) {
-        if (minc >= INF64) g.ctl->infeasible = 1;
-        else np = pv - (minc + eps);
-        c.relabel++;
-    }
-    PN[v] = np;
-    act |= (pushed > 0) | (rem > 0);
-}
-
-__device__ __forceinline__ void medium_discharge(const DG& g, int v, const long long* __restrict__ P,
-                                                 long long* __restrict__ PN, long long eps, Pend& pd, int& act,
-                                                 Cnt& c) {
-    const int lane = lane_id();
-    const long long e = g.excess[v];
-    if (e <= 0) return;
-    if (lane == 0) c.visit++;
-    const long long pv = P[v];
     long long rem = e, minc = INF64;
-    const int b = g.first[v], en = g.first[v + 1];
-    for (int base = b; base < en; base += WAVE) {
-        const int a = base + lane;
+    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;   // G == 64: one node per wave
+    for (int it = 0; it < iters; ++it) {
+        const int a = b0 + it * G + lig;
         const bool valid = a < en;
         long long r = 0, cr = 0;
         int w = 0;
@@ -497,14 +589,14 @@ __device__ __forceinline__ void medium_discharge(const DG& g, int v, const long 
             c.scan++;
         }
         const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
-        const long long incl = wave_incl_scan(adm, lane);
-        const long long total = __shfl(incl, WAVE - 1);
+        const long long incl = g_incl_scan<G>(adm);
+        const long long total = __shfl(incl, G - 1, G);
         long long d = rem - (incl - adm);
         d = d < 0 ? 0 : (d > adm ? adm : d);
         if (d > 0) {
             g.rcap[a] = r - d;
             g.rcap[g.rev[a]] += d;
-            push_excess(g, w, d, pd);
+            push_excess(g, &nf, w, d, pd, out);
             c.push++;
         }
         if (valid) {
@@ -516,24 +608,22 @@ __device__ __forceinline__ void medium_discharge(const DG& g, int v, const long 
         }
         rem -= total < rem ? total : rem;
         flush_pending(g, pd);
-        if (rem == 0) break;
+        if (G == 64 && rem == 0) break;
     }
-    if (lane == 0) {
+    minc = g_min<G>(minc);
+    if (act && lig == 0) {
         const long long pushed = e - rem;
         if (pushed) atom_add(&g.excess[v], -pushed);
-    }
-    long long np = pv;
-    if (rem > 0) {
-        minc = wave_min(minc);
-        if (minc >= INF64) {
-            if (lane == 0) g.ctl->infeasible = 1;
-        } else {
-            np = pv - (minc + eps);
+        long long np = pv;
+        if (rem > 0) {
+            if (minc >= INF64) g.ctl->infeasible = 1;
+            else np = pv - (minc + eps);
+            c.relabel++;
+            nf.flag[g.fidx[v]] = 1;   // still active next sweep
+            out = 1;
         }
-        if (lane == 0) c.relabel++;
+        PN[v] = np;
     }
-    if (lane == 0) PN[v] = np;
-    act |= (e - rem > 0) | (rem > 0);
 }
 
 __device__ long long heavy_claim(long long* ex, long long want) {
@@ -548,15 +638,13 @@ __device__ long long heavy_claim(long long* ex, long long want) {
     }
 }
 
-__device__ void heavy_chunk(const DG& g, const HItem& it, const long long* __restrict__ P,
-                            long long* __restrict__ PN, long long eps, Pend& pd, int& act, Cnt& c) {
+__device__ void heavy_chunk(const DG& g, const Front& nf, const HItem& it, const long long* __restrict__ P,
+                            long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
     const int x = it.node, h = it.hid;
     const bool chunk0 = it.begin == g.first[x];
-    if (chunk0 && threadIdx.x == 0) {
-        if (drain_inbox(g, h, x)) act = 1;
-    }
+    if (chunk0 && threadIdx.x == 0) drain_inbox(g, h, x);
     const long long px = P[x];
     long long r[PER_T], cr[PER_T], adm[PER_T];
     int w[PER_T];
@@ -592,9 +680,8 @@ __device__ void heavy_chunk(const DG& g, const HItem& it, const long long* __res
         if (d > 0) {
             g.rcap[a] = r[k] - d;
             g.rcap[g.rev[a]] += d;
-            push_excess(g, w[k], d, pd);
+            push_excess(g, &nf, w[k], d, pd, out);
             c.push++;
-            act = 1;
         }
         if (a < it.end) {
             if (cr[k] < 0) {
@@ -623,7 +710,8 @@ __device__ void heavy_chunk(const DG& g, const HItem& it, const long long* __res
                 c.relabel++;
             }
             if (ex > 0) {
-                act = 1;
+                nf.hub[h] = 1;
+                out = 1;
                 c.visit++;
             }
             PN[x] = np;
@@ -632,132 +720,151 @@ __device__ void heavy_chunk(const DG& g, const HItem& it, const long long* __res
     }
 }
 
-__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int tidx) {
-    const int prev = pos ? g.ctl->active[pos - 1] : g.ctl->active_prev;
-    if (!prev) return;
+__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx) {
+    if (blockIdx.x == 0)
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
+    if (!g.ctl->bf_done) return;   // the preceding global update has not been applied
+    if (!(pos == 0 ? g.ctl->apply_act : g.ctl->sweep_act[pos - 1])) return;   // empty frontier
+    const Front F = g.sf[seq % 3], N = g.sf[(seq + 1) % 3];
     const long long eps = g.ctl->eps;
     const long long* P = (pos & 1) ? g.p1 : g.p0;
     long long* PN = (pos & 1) ? g.p0 : g.p1;
     Pend pd{-1, 0};
     Cnt c;
-    int act = 0;
-    int b = blockIdx.x;
-    if (b < g.nhitems) {
-        heavy_chunk(g, g.hitems[b], P, PN, eps, pd, act, c);
+    int out = 0;
+    if ((int)blockIdx.x < g.nhitems) {
+        const HItem it = g.hitems[blockIdx.x];
+        if (F.hub[it.hid]) heavy_chunk(g, N, it, P, PN, eps, pd, out, c);
     } else {
-        b -= g.nhitems;
-        if (b < g.nmblocks) {
-            const int wi = b * WPB + (threadIdx.x >> 6);
-            if (wi < g.nmedium) medium_discharge(g, g.medium[wi], P, PN, eps, pd, act, c);
-            flush_pending(g, pd);
-        } else {
-            b -= g.nmblocks;
-            const int i = b * BLK + threadIdx.x;
-            if (i < g.nlight) light_discharge(g, g.light[i], P, PN, eps, pd, act, c);
-            flush_pending(g, pd);
-        }
+        const Scan sc{F.flag, 0};
+#define KS_SWEEP_CALL(C) sweep_group<G_>(g, N, v, P, PN, eps, pd, out, c)
+        KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SWEEP_CALL)
+#undef KS_SWEEP_CALL
     }
-    if (__any(act) && lane_id() == 0) g.ctl->active[pos] = 1;
+    if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
     if (g.trace && tidx >= 0) {
         const long long v = wave_sum(c.visit), r = wave_sum(c.relabel);
         if (lane_id() == 0 && (v | r)) {
-            const int cls = blockIdx.x < g.nhitems ? 3 : (blockIdx.x < g.nhitems + g.nmblocks ? 2 : -1);
+            const int cls = (int)blockIdx.x < g.nhitems ? 3 : 2;
             atomicAdd(&g.trace[4 * tidx], (unsigned)v);
             atomicAdd(&g.trace[4 * tidx + 1], (unsigned)r);
-            if (cls > 0) atomicAdd(&g.trace[4 * tidx + cls], (unsigned)v);
+            atomicAdd(&g.trace[4 * tidx + cls], (unsigned)v);
         }
     }
     flush_counters(g, c);
 }
 
-// ===================================================== global price update ===
-// Distances (in ε units) from the deficit nodes over residual arcs with length
-// floor(rc/ε)+1 (clamped), by label-correcting Bellman-Ford sweeps.
-__global__ void k_gu_init(DG g) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
-        g.dist[v] = g.excess[v] < 0 ? 0 : INF64;
-}
-
-__device__ __forceinline__ long long relax_arc(const DG& g, int a, long long pu, const long long* __restrict__ P,
-                                               long long eps) {
-    if (g.rcap[a] <= 0) return INF64;
-    const int v = g.head[a];
-    const long long dv = g.dist[v];
-    if (dv >= INF64) return INF64;
-    long long len = floordiv(g.cost[a] + pu - P[v], eps) + 1;
-    len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
+// ================================================ Bellman-Ford (GU and PR) ===
+// Global price update (GU): distances from the deficit nodes over residual arcs
+// of length clamp(floor(rc/ε)+1, 0, LEN_CAP), unreached = INF.
+// Price refinement (PR): all distances start at 0, lengths floor(rc/ε)+1 may be
+// negative (difference constraints of ε-optimality).
+// Push-style: a node whose distance dropped relaxes its IN-arcs (u→v), found as
+// the reverses of its CSR arcs (cost(u→v) = −cost(v→u)). No returning atomics:
+// a plain pre-check filters (a stale distance is only larger), atomicMin
+// commits, the flag store marks u for the next round.
+template <bool PR>
+__device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
+                                         long long eps, long long* hub_min, int& out) {
+    const int ra = g.rev[a];
+    if (g.rcap[ra] <= 0) return;
+    const int u = g.head[a];
+    const long long cr = -g.cost[a] + g.p0[u] - pv;
+    long long len = floordiv(cr, eps) + 1;
+    if (!PR) len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
     const long long cand = dv + len;
-    return cand < INF64 ? cand : INF64;
+    const int h = g.hidx[u];
+    if (h >= 0 && h < HUB_LDS) {
+        __hip_atomic_fetch_min(&hub_min[h], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    if (cand >= g.dist[u]) return;
+    atom_min(&g.dist[u], cand);
+    if (h >= 0) nf.hub[h] = 1;
+    else nf.flag[g.fidx[u]] = 1;
+    out = 1;
 }
 
-__global__ __launch_bounds__(BLK) void k_gu_relax(DG g, int pos) {
-    const int prev = pos ? g.ctl->gu_changed[pos - 1] : g.ctl->gu_prev;
-    if (!prev) return;
+template <int G, bool PR>
+__device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long* hub_min,
+                                         int& out, long long& scans) {
+    const int lig = lane_id() & (G - 1);
+    long long dv = INF64;
+    if (v >= 0) dv = g.dist[v];
+    const bool act = v >= 0 && (PR || dv < INF64);
+    long long pv = 0;
+    int b0 = 0, en = 0;
+    if (act) {
+        pv = g.p0[v];
+        b0 = g.first[v];
+        en = g.first[v + 1];
+    }
+    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
+    for (int it = 0; it < iters; ++it) {
+        const int a = b0 + it * G + lig;
+        if (a < en) {
+            relax_in<PR>(g, nf, a, dv, pv, eps, hub_min, out);
+            scans++;
+        }
+    }
+}
+
+// One Bellman-Ford round. dense = 1: every node (first round of an update).
+template <bool PR>
+__global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
+    __shared__ long long hub_min[HUB_LDS];
+    if (blockIdx.x == 0) {
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.bf[(seq + 2) % 3].hub[h] = 0;
+        if (threadIdx.x == 0) g.ctl->bfa[(seq + 2) % 3] = 0;
+    }
+    if (g.ctl->bf_done) return;
+    if (!dense && !g.ctl->bfa[seq % 3]) {   // empty frontier: the update converged
+        if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->bf_done = 1;
+        return;
+    }
+    const Front F = g.bf[seq % 3], N = g.bf[(seq + 1) % 3];
+    if (threadIdx.x < HUB_LDS) hub_min[threadIdx.x] = INF64;
+    __syncthreads();
     const long long eps = g.ctl->eps;
-    const long long* P = g.p0;
-    int changed = 0;
+    int out = 0;
     long long scans = 0;
-    int b = blockIdx.x;
-    if (b < g.nhitems) {
-        __shared__ long long sh[WPB];
-        const HItem it = g.hitems[b];
-        const long long pu = P[it.node];
-        long long best = INF64;
-        for (int k = 0; k < PER_T; ++k) {
-            const int a = it.begin + threadIdx.x * PER_T + k;
-            if (a < it.end) {
-                best = min(best, relax_arc(g, a, pu, P, eps));
-                scans++;
-            }
-        }
-        best = block_min(best, sh);
-        if (threadIdx.x == 0 && best < INF64) {
-            const long long old = atom_min_ret(&g.dist[it.node], best);
-            if (best < old) changed = 1;
-        }
-    } else {
-        b -= g.nhitems;
-        if (b < g.nmblocks) {
-            const int wi = b * WPB + (threadIdx.x >> 6);
-            if (wi < g.nmedium) {
-                const int u = g.medium[wi];
-                const long long du = g.dist[u];
-                if (du > 0) {
-                    const long long pu = P[u];
-                    long long best = INF64;
-                    const int e = g.first[u + 1];
-                    for (int a = g.first[u] + lane_id(); a < e; a += WAVE) {
-                        best = min(best, relax_arc(g, a, pu, P, eps));
+    if ((int)blockIdx.x < g.nhitems) {
+        const HItem it = g.hitems[blockIdx.x];
+        if (dense || F.hub[it.hid]) {
+            const long long dv = atom_load(&g.dist[it.node]);
+            if (PR || dv < INF64) {
+                const long long pv = g.p0[it.node];
+                for (int k = 0; k < PER_T; ++k) {
+                    const int a = it.begin + threadIdx.x * PER_T + k;
+                    if (a < it.end) {
+                        relax_in<PR>(g, N, a, dv, pv, eps, hub_min, out);
                         scans++;
                     }
-                    best = wave_min(best);
-                    if (best < du) {
-                        if (lane_id() == 0) g.dist[u] = best;
-                        changed = 1;
-                    }
                 }
             }
-        } else {
-            b -= g.nmblocks;
-            const int i = b * BLK + threadIdx.x;
-            if (i < g.nlight) {
-                const int u = g.light[i];
-                const long long du = g.dist[u];
-                if (du > 0) {
-                    const long long pu = P[u];
-                    long long best = INF64;
-                    const int e = g.first[u + 1];
-                    for (int a = g.first[u]; a < e; ++a) best = min(best, relax_arc(g, a, pu, P, eps));
-                    scans += e - g.first[u];
-                    if (best < du) {
-                        g.dist[u] = best;
-                        changed = 1;
-                    }
-                }
+        }
+    } else {
+        const Scan sc{F.flag, dense};
+#define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, hub_min, out, scans)
+        KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_BF_CALL)
+#undef KS_BF_CALL
+    }
+    __syncthreads();
+    if (threadIdx.x < HUB_LDS && (int)threadIdx.x < g.nheavy) {
+        const long long val = hub_min[threadIdx.x];
+        if (val < INF64) {
+            const long long old = atom_min_ret(&g.dist[g.hnode[threadIdx.x]], val);
+            if (val < old) {
+                N.hub[threadIdx.x] = 1;
+                out = 1;
             }
         }
     }
-    if (__any(changed) && lane_id() == 0) g.ctl->gu_changed[pos] = 1;
+    if (__any(out) && lane_id() == 0) g.ctl->bfa[(seq + 1) % 3] = 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(g.ctr + C_BFROUND, 1ULL);
+        g.ctl->bf_count += 1;
+    }
     scans = wave_sum(scans);
     if (lane_id() == 0 && scans) {
         const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
@@ -765,9 +872,53 @@ __global__ __launch_bounds__(BLK) void k_gu_relax(DG g, int pos) {
     }
 }
 
-// per-block max of finite distances
-__global__ void k_gu_maxd(DG g, long long* __restrict__ part) {
+__device__ __forceinline__ void clear_fronts(const DG& g, const Front* fs) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < g.n_pad; i += (long long)gridDim.x * BLK) {
+        fs[0].flag[i] = 0;
+        fs[1].flag[i] = 0;
+        fs[2].flag[i] = 0;
+    }
+    if (blockIdx.x == 0)
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) fs[0].hub[h] = fs[1].hub[h] = fs[2].hub[h] = 0;
+}
+
+// GU init: drain hub inboxes, dist = 0 at deficits / INF elsewhere, clean flags.
+__global__ void k_gu_init(DG g) {
+    clear_fronts(g, g.bf);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g.ctl->bf_done = 0;
+        g.ctl->gu_L = 0;
+        g.ctl->bfa[0] = g.ctl->bfa[1] = g.ctl->bfa[2] = 0;
+    }
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
+        const int h = g.hidx[v];
+        if (h >= 0) drain_inbox(g, h, (int)v);
+        const long long e = h >= 0 ? atom_load(&g.excess[v]) : g.excess[v];
+        g.dist[v] = e < 0 ? 0 : INF64;
+    }
+}
+
+// PR init: dist = 0 everywhere.
+__global__ void k_pr_init(DG g) {
+    clear_fronts(g, g.bf);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g.ctl->bf_done = 0;
+        g.ctl->bfa[0] = g.ctl->bfa[1] = g.ctl->bfa[2] = 0;
+    }
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
+        g.dist[v] = 0;
+}
+
+// max finite distance (only once the update converged); cleans the sweep
+// frontiers and flags the apply step and the sweeps write.
+__global__ void k_gu_max(DG g) {
     __shared__ long long sh[WPB];
+    clear_fronts(g, g.sf);
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < MAXB; k += BLK) g.ctl->sweep_act[k] = 0;
+        if (threadIdx.x == 0) g.ctl->apply_act = 0;
+    }
+    if (!g.ctl->bf_done) return;
     long long mx = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = g.dist[v];
@@ -780,27 +931,38 @@ __global__ void k_gu_maxd(DG g, long long* __restrict__ part) {
     if (threadIdx.x == 0) {
         long long t = 0;
         for (int i = 0; i < WPB; ++i) t = max(t, sh[i]);
-        part[blockIdx.x] = t;
+        if (t) __hip_atomic_fetch_max(&g.ctl->gu_L, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-__global__ void k_gu_apply(DG g, const long long* __restrict__ part, int nparts) {
-    __shared__ long long s_dt;
-    if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int i = 0; i < nparts; ++i) t = max(t, part[i]);
-        const long long eps = g.ctl->eps;
-        const long long lim = (1LL << 60) / eps;
-        s_dt = t < lim ? t : lim;
-    }
-    __syncthreads();
-    const long long dt = s_dt;
+// apply p ← p − ε·min(d, L) and seed the sweep frontier with every excess node.
+__global__ void k_gu_apply(DG g, int sseq) {
+    if (!g.ctl->bf_done) return;
     const long long eps = g.ctl->eps;
+    const long long lim = (1LL << 60) / eps;
+    long long L = g.ctl->gu_L;
+    L = L < lim ? L : lim;
+    const Front F = g.sf[sseq % 3];
+    int out = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = g.dist[v];
-        if (d >= INF64 && g.excess[v] > 0) g.ctl->infeasible = 1;
-        const long long dd = d < dt ? d : dt;
+        const long long e = g.excess[v];
+        if (d >= INF64 && e > 0) g.ctl->infeasible = 1;
+        const long long dd = d < L ? d : L;
         const long long np = g.p0[v] - eps * dd;
+        g.p0[v] = np;
+        g.p1[v] = np;
+        if (e > 0) mark(g, F, (int)v, out);
+    }
+    if (__any(out) && lane_id() == 0) g.ctl->apply_act = 1;
+}
+
+// PR success: p ← p − ε·d (d ≤ 0).
+__global__ void k_pr_apply(DG g) {
+    if (!g.ctl->bf_done) return;
+    const long long eps = g.ctl->eps;
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
+        const long long np = g.p0[v] - eps * g.dist[v];
         g.p0[v] = np;
         g.p1[v] = np;
     }
@@ -808,6 +970,11 @@ __global__ void k_gu_apply(DG g, const long long* __restrict__ part, int nparts)
 
 // ================================================================ verify ===
 // Conservation, capacity and 1-optimality (scaled units); per-block cost sums.
+__global__ void k_drain_all(DG g) {
+    const int h = blockIdx.x * BLK + threadIdx.x;
+    if (h < g.nheavy) drain_inbox(g, h, g.hnode[h]);
+}
+
 __global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const long long* __restrict__ low,
                               const long long* __restrict__ cap, const long long* __restrict__ cost,
                               long long* __restrict__ flows, long long* __restrict__ part) {
@@ -891,7 +1058,6 @@ struct EngineImpl {
     ks_opts opts{};
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
-    hipEvent_t kev[4] = {};   // kernel-batch timing (sweeps, relaxations)
 
     // input (compacted) graph
     int64_t n = 0, m = 0;
@@ -905,8 +1071,12 @@ struct EngineImpl {
     DBuf<unsigned char> sort_tmp;
     DBuf<int> first, head, rev, fwd;
     DBuf<long long> rcap, scost, excess, p0, p1, dist;
+    DBuf<int> order, fidx;
+    DBuf<unsigned char> flags;   // 6 frontier buffers × n_pad
+    DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned char> cls;
-    DBuf<int> hidx, light, medium, heavy, nsel;
+    DBuf<int> hidx, nsel;
+    DBuf<int> cls_list[NGC + 1];   // every node of each degree class; [NGC] = heavy hubs
     DBuf<unsigned char> sel_tmp;
     DBuf<HItem> hitems;
     DBuf<int> hnchunks, harrive, hunsat;
@@ -915,8 +1085,11 @@ struct EngineImpl {
     DBuf<unsigned> trace;
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;       // pinned host mirror
-    long long* h_scr = nullptr; // pinned scratch: [0] eps, [1] constant 1
-    int nlight = 0, nmedium = 0, nheavy = 0, nhitems = 0;
+    long long* h_scr = nullptr; // pinned scratch: [0] eps
+    int ncls[NGC + 1] = {0};
+    int n_pad = 0;
+    int obeg[NGC + 1] = {0}, wbeg[NGC + 1] = {0};
+    int nheavy = 0, nhitems = 0;
     bool solved = false;
 
     ~EngineImpl() {
@@ -928,17 +1101,18 @@ struct EngineImpl {
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release();
         sort_tmp.release(); first.release(); head.release(); rev.release(); fwd.release();
         rcap.release(); scost.release(); excess.release(); p0.release(); p1.release(); dist.release();
-        cls.release(); hidx.release(); light.release(); medium.release(); heavy.release(); nsel.release();
-        sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release(); hunsat.release();
-        hmin.release(); inbox.release(); part.release(); flows.release(); ctr.release(); trace.release(); ctl.release();
+        order.release(); fidx.release(); flags.release(); hubflags.release(); cls.release(); hidx.release();
+        for (auto& b : cls_list) b.release();
+        nsel.release(); sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release();
+        hunsat.release(); hmin.release(); inbox.release(); part.release(); flows.release();
+        ctr.release(); trace.release(); ctl.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
-        for (auto& e : kev)
-            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
+
 
     DG dg() const {
         DG g{};
@@ -952,30 +1126,36 @@ struct EngineImpl {
         g.excess = excess.p;
         g.p0 = p0.p;
         g.p1 = p1.p;
+        g.dist = dist.p;
+        g.order = order.p;
+        g.fidx = fidx.p;
+        g.n_pad = n_pad;
+        for (int c = 0; c <= NGC; ++c) {
+            g.obeg[c] = obeg[c];
+            g.wbeg[c] = wbeg[c];
+        }
         g.hidx = hidx.p;
         g.inbox = inbox.p;
-        g.light = light.p;
-        g.nlight = nlight;
-        g.medium = medium.p;
-        g.nmedium = nmedium;
         g.hitems = hitems.p;
         g.nhitems = nhitems;
         g.nheavy = nheavy;
-        g.hnode = heavy.p;
+        g.hnode = cls_list[NGC].p;
         g.hnchunks = hnchunks.p;
         g.harrive = harrive.p;
         g.hmin = hmin.p;
         g.hunsat = hunsat.p;
-        g.dist = dist.p;
+        const int hs = std::max(1, nheavy);
+        for (int k = 0; k < 6; ++k) {
+            Front f{flags.p + (size_t)k * n_pad, hubflags.p + (size_t)k * hs};
+            if (k < 3) g.sf[k] = f;
+            else g.bf[k - 3] = f;
+        }
         g.ctl = ctl.p;
         g.ctr = ctr.p;
-        g.trace = trace.n ? trace.p : nullptr;
-        g.nmblocks = (nmedium + WPB - 1) / WPB;
+        g.trace = trace.n > 1 ? trace.p : nullptr;
         return g;
     }
-    int sweep_grid() const {
-        return std::max(1, nhitems + (nmedium + WPB - 1) / WPB + (nlight + BLK - 1) / BLK);
-    }
+    int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
 };
 
 #define KS_CHECK(expr)                                                   \
@@ -1004,12 +1184,10 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     KS_CHECK(hipSetDevice(device));
     KS_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
-    for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
     KS_CHECK(hipHostMalloc(&s.h_scr, 4 * sizeof(long long)));
-    s.h_scr[1] = 1;
     return KS_OK;
 }
 
@@ -1017,7 +1195,7 @@ int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
                    const int64_t* cap, const int64_t* cost, const int64_t* supply, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
-    if (n < 0 || m < 0 || n > (1LL << 30) || m > (1LL << 29)) {
+    if (n < 0 || m < 0 || n > (1LL << 29) || m > (1LL << 29)) {
         err = "graph too large for 32-bit CSR indices";
         return KS_E_RANGE;
     }
@@ -1064,6 +1242,9 @@ int Engine::solve(ks_result& res, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
     const auto t_host0 = std::chrono::steady_clock::now();
+    auto wall_s = [&]() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count();
+    };
     hipStream_t st = s.stream;
     const int64_t n = s.n, m = s.m, m2 = 2 * m;
     s.solved = false;
@@ -1098,25 +1279,28 @@ int Engine::solve(ks_result& res, std::string& err) {
     KS_CHECK(s.p0.ensure(n));
     KS_CHECK(s.p1.ensure(n));
     KS_CHECK(s.dist.ensure(n));
+    KS_CHECK(s.fidx.ensure(n));
     KS_CHECK(s.cls.ensure(n));
     KS_CHECK(s.hidx.ensure(n));
-    KS_CHECK(s.light.ensure(n));
-    KS_CHECK(s.medium.ensure(n));
-    KS_CHECK(s.heavy.ensure(n));
-    KS_CHECK(s.nsel.ensure(4));
+    for (auto& b : s.cls_list) KS_CHECK(b.ensure(n));
+    KS_CHECK(s.nsel.ensure(NGC + 1));
     KS_CHECK(s.flows.ensure(m));
     KS_CHECK(s.part.ensure(4096));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
+    std::memset(s.h_ctl, 0, sizeof(Ctl));
     const char* trace_path = std::getenv("KS_TRACE");
     if (trace_path && *trace_path) {
         KS_CHECK(s.trace.ensure(4 * kTraceMax));
         KS_CHECK(hipMemsetAsync(s.trace.p, 0, 4 * kTraceMax * sizeof(unsigned), st));
+    } else {
+        s.trace.release();
     }
     struct PhaseRec {
         long long eps;
         uint64_t begin, end;
         std::vector<uint64_t> gu_at;
+        int pr_rounds;   // price-refinement rounds; > 0 success (phase skipped), < 0 failed
     };
     std::vector<PhaseRec> ptrace;
 
@@ -1140,41 +1324,36 @@ int Engine::solve(ks_result& res, std::string& err) {
     hipLaunchKernelGGL(k_first, dim3(grid_for(n + 1)), dim3(BLK), 0, st, (int)n, (long long)m2, s.keys_out.p,
                        s.first.p);
     hipLaunchKernelGGL(k_node_init, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, s.supply.p, s.first.p,
-                       s.excess.p, s.p0.p, s.p1.p, s.cls.p, s.hidx.p);
+                       s.excess.p, s.p0.p, s.p1.p, s.cls.p, s.hidx.p, s.fidx.p);
     if (m)
         hipLaunchKernelGGL(k_lower_bounds, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
                            s.a_low.p, s.excess.p);
     {
         hipcub::CountingInputIterator<int> it(0);
         size_t tmp = 0, t2 = 0;
-        for (unsigned char c = 0; c < 3; ++c) {
-            KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.light.p, s.nsel.p + c, (int)n,
+        for (unsigned char c = 0; c <= NGC; ++c) {
+            KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)n,
                                               ClassIs{s.cls.p, c}, st));
             tmp = std::max(tmp, t2);
         }
         KS_CHECK(s.sel_tmp.ensure(tmp));
-        int* outs[3] = {s.light.p, s.medium.p, s.heavy.p};
-        for (unsigned char c = 0; c < 3; ++c) {
+        for (unsigned char c = 0; c <= NGC; ++c) {
             t2 = tmp;
-            KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, outs[c], s.nsel.p + c, (int)n,
+            KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)n,
                                               ClassIs{s.cls.p, c}, st));
         }
     }
-    int counts[4] = {0, 0, 0, 0};
-    KS_CHECK(hipMemcpyAsync(counts, s.nsel.p, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipMemcpyAsync(s.ncls, s.nsel.p, (NGC + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
     KS_CHECK(hipStreamSynchronize(st));
-    s.nlight = counts[0];
-    s.nmedium = counts[1];
-    s.nheavy = counts[2];
+    s.nheavy = s.ncls[NGC];
     {
         // heavy hubs: chunk table (few hubs; built on host from their CSR ranges)
         std::vector<int> hn(s.nheavy), hf(2 * s.nheavy);
         if (s.nheavy) {
-            KS_CHECK(hipMemcpyAsync(hn.data(), s.heavy.p, s.nheavy * sizeof(int), hipMemcpyDeviceToHost, st));
+            KS_CHECK(hipMemcpyAsync(hn.data(), s.cls_list[NGC].p, s.nheavy * sizeof(int), hipMemcpyDeviceToHost, st));
             KS_CHECK(hipStreamSynchronize(st));
-            for (int h = 0; h < s.nheavy; ++h) {
+            for (int h = 0; h < s.nheavy; ++h)
                 KS_CHECK(hipMemcpyAsync(&hf[2 * h], s.first.p + hn[h], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-            }
             KS_CHECK(hipStreamSynchronize(st));
         }
         std::vector<HItem> items;
@@ -1192,6 +1371,28 @@ int Engine::solve(ks_result& res, std::string& err) {
         KS_CHECK(s.hunsat.ensure(s.nheavy));
         KS_CHECK(s.hmin.ensure(s.nheavy));
         KS_CHECK(s.inbox.ensure((size_t)s.nheavy * SHARDS));
+        // class-ordered slots, each class padded to whole 64-slot windows
+        int o = 0, wv = 0;
+        for (int c = 0; c < NGC; ++c) {
+            s.obeg[c] = o;
+            s.wbeg[c] = wv;
+            const int pad = (s.ncls[c] + 63) / 64 * 64;
+            o += pad;
+            wv += pad / win_slots(c);
+        }
+        s.obeg[NGC] = o;
+        s.wbeg[NGC] = wv;
+        s.n_pad = o;
+        KS_CHECK(s.order.ensure(std::max(1, o)));
+        KS_CHECK(s.flags.ensure(6 * (size_t)std::max(1, o)));
+        KS_CHECK(s.hubflags.ensure(6 * (size_t)std::max(1, s.nheavy)));
+        KS_CHECK(hipMemsetAsync(s.order.p, 0xff, std::max(1, o) * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.flags.p, 0, 6 * (size_t)std::max(1, o), st));
+        KS_CHECK(hipMemsetAsync(s.hubflags.p, 0, 6 * (size_t)std::max(1, s.nheavy) * sizeof(int), st));
+        for (int c = 0; c < NGC; ++c)
+            if (s.ncls[c])
+                hipLaunchKernelGGL(k_make_order, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c], s.obeg[c],
+                                   (const int*)s.cls_list[c].p, s.order.p, s.fidx.p);
         if (s.nheavy) {
             std::vector<long long> hm(s.nheavy, INF64);
             KS_CHECK(hipMemcpyAsync(s.hitems.p, items.data(), items.size() * sizeof(HItem), hipMemcpyHostToDevice, st));
@@ -1200,8 +1401,8 @@ int Engine::solve(ks_result& res, std::string& err) {
             KS_CHECK(hipMemsetAsync(s.harrive.p, 0, s.nheavy * sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.hunsat.p, 0, s.nheavy * sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.inbox.p, 0, (size_t)s.nheavy * SHARDS * sizeof(long long), st));
-            hipLaunchKernelGGL(k_set_hidx, dim3((s.nheavy + BLK - 1) / BLK), dim3(BLK), 0, st, s.nheavy, s.heavy.p,
-                               s.hidx.p);
+            hipLaunchKernelGGL(k_set_hidx, dim3((s.nheavy + BLK - 1) / BLK), dim3(BLK), 0, st, s.nheavy,
+                               s.cls_list[NGC].p, s.hidx.p);
             KS_CHECK(hipStreamSynchronize(st));
         }
     }
@@ -1209,18 +1410,20 @@ int Engine::solve(ks_result& res, std::string& err) {
 
     // ------------------------------------------------------------ phases ---
     DG g = s.dg();
-    const int sgrid = s.sweep_grid();
-    const int K = std::max(2, std::min(MAXB, s.opts.sweeps_per_batch > 0 ? s.opts.sweeps_per_batch : 32)) & ~1;
-    const int GK = 16;
-    const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
-    const int gu_interval = s.opts.gu_interval > 0 ? s.opts.gu_interval : 48;
+    const int fgrid = s.window_grid();
+    const int dgrid = fgrid;
     const int ngrid = grid_for(n, 2048);
+    const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
+    int gi = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
+    gi = std::max(2, std::min(MAXB, gi)) & ~1;     // even: sweeps end on p0
+    const int pr_cap = 160;             // price-refinement rounds before giving up
+    const bool use_pr = s.opts.price_refine != 0;
     long long eps = std::max<long long>(1, (long long)s.maxc * mult);
-    uint64_t sweeps = 0, gus = 0, gu_iters = 0, sweep_launches = 0, gu_launches = 0;
-    double ms_sweep_k = 0, ms_gu_k = 0;
-    int phases = 0;
-    double ms_sat = 0, ms_sweep = 0, ms_gu = 0;
-    const int* one = reinterpret_cast<const int*>(&s.h_scr[1]);
+    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, cycles = 0;
+    int phases = 0, pr_skips = 0;
+    int kb = 24;                        // Bellman-Ford rounds enqueued per cycle (adaptive)
+    int sseq = 0, bseq = 0;             // frontier buffer sequences
+    double ms_sat = 0, ms_cycles = 0, ms_pr = 0;
     int status = KS_OK;
 
     auto read_ctl = [&]() -> hipError_t {
@@ -1228,92 +1431,101 @@ int Engine::solve(ks_result& res, std::string& err) {
         if (e != hipSuccess) return e;
         return hipStreamSynchronize(st);
     };
-
-    auto global_update = [&]() -> int {
-        hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
-        hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g);
-        for (int rounds = 0;; ++rounds) {
-            KS_CHECK(hipMemsetAsync(s.ctl.p->gu_changed, 0, sizeof(int) * GK, st));
-            KS_CHECK(hipMemcpyAsync(&s.ctl.p->gu_prev, one, sizeof(int), hipMemcpyHostToDevice, st));
-            KS_CHECK(hipEventRecord(s.kev[0], st));
-            for (int k = 0; k < GK; ++k) hipLaunchKernelGGL(k_gu_relax, dim3(sgrid), dim3(BLK), 0, st, g, k);
-            KS_CHECK(hipEventRecord(s.kev[1], st));
+    auto set_eps = [&](long long e) -> hipError_t {
+        s.h_scr[0] = e;
+        return hipMemcpyAsync(&s.ctl.p->eps, &s.h_scr[0], sizeof(long long), hipMemcpyHostToDevice, st);
+    };
+    auto bf_rounds = [&](bool pr, int k, bool first_dense) {
+        for (int r = 0; r < k; ++r) {
+            const int dense = (first_dense && r == 0) ? 1 : 0;
+            const int grid = dense ? dgrid : fgrid;
+            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
+            else hipLaunchKernelGGL(k_bf_round<false>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
+            ++bseq;
+            ++bf_launches;
+        }
+    };
+    // Price refinement at eps_try: 1 = success (prices updated), 0 = failed, <0 error.
+    auto price_refine = [&](long long eps_try, int* rounds_used) -> int {
+        KS_CHECK(hipEventRecord(s.ev[6], st));
+        KS_CHECK(set_eps(eps_try));
+        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g);
+        int used = 0, ok = 0;
+        for (int batch = 0; used < pr_cap; ++batch) {
+            const int k = std::min(64, pr_cap - used);
+            bf_rounds(true, k, batch == 0);
+            used += k;
             KS_CHECK(read_ctl());
-            gu_launches += GK;
-            ms_gu_k += ev_ms(s.kev[0], s.kev[1]);
-            int it = 0;
-            for (int k = 0; k < GK; ++k) it += s.h_ctl->gu_changed[k] ? 1 : 0;
-            gu_iters += it;
-            if (!s.h_ctl->gu_changed[GK - 1]) break;
-            if (rounds > 1 + (int)(4 * n / GK) ||
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count() >
-                    kSolveWallLimitS) {
-                err = "global price update did not converge";
-                return KS_E_DEVICE;
+            if (s.h_ctl->bf_done) {
+                ok = 1;
+                break;
             }
         }
-        hipLaunchKernelGGL(k_gu_maxd, dim3(ngrid), dim3(BLK), 0, st, g, s.part.p);
-        hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, (const long long*)s.part.p, ngrid);
-        ++gus;
-        return KS_OK;
+        if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g);
+        KS_CHECK(hipEventRecord(s.ev[7], st));
+        KS_CHECK(hipEventSynchronize(s.ev[7]));
+        ms_pr += ev_ms(s.ev[6], s.ev[7]);
+        *rounds_used = used;
+        return ok;
     };
 
     do {
         eps = std::max<long long>(1, eps / alpha);
         ++phases;
-        s.h_scr[0] = eps;
-        KS_CHECK(hipMemcpyAsync(&s.ctl.p->eps, &s.h_scr[0], sizeof(long long), hipMemcpyHostToDevice, st));
+        ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}, 0});
+        KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(sgrid), dim3(BLK), 0, st, g);
+        hipLaunchKernelGGL(k_saturate, dim3(dgrid), dim3(BLK), 0, st, g);
         KS_CHECK(hipEventRecord(s.ev[3], st));
-        ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}});
-        int rc = global_update();
-        if (rc) return rc;
-        KS_CHECK(hipEventRecord(s.ev[4], st));
+        bool gu_running = false;
         uint64_t phase_sweeps = 0;
-        int since_gu = 0;
+        int gu_r0 = 0;   // bf_count when the running update started
         for (;;) {
-            KS_CHECK(hipMemsetAsync(s.ctl.p->active, 0, sizeof(int) * K, st));
-            KS_CHECK(hipMemcpyAsync(&s.ctl.p->active_prev, one, sizeof(int), hipMemcpyHostToDevice, st));
-            KS_CHECK(hipEventRecord(s.kev[2], st));
-            for (int k = 0; k < K; ++k) {
+            // one cycle: [GU init] [kb BF rounds] [max] [apply] [gi sweeps]
+            const bool new_gu = !gu_running;
+            if (new_gu) {
+                gu_r0 = s.h_ctl->bf_count;
+                hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g);
+                ptrace.back().gu_at.push_back(sweep_launches);
+            }
+            bf_rounds(false, kb, new_gu);
+            hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
+            hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
+            for (int k = 0; k < gi; ++k) {
                 const long long ti = (long long)sweep_launches + k;
-                hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k,
+                hipLaunchKernelGGL(k_sweep, dim3(fgrid), dim3(BLK), 0, st, g, k, sseq + k,
                                    (g.trace && ti < kTraceMax) ? (int)ti : -1);
             }
-            KS_CHECK(hipEventRecord(s.kev[3], st));
             KS_CHECK(read_ctl());
-            sweep_launches += K;
-            ms_sweep_k += ev_ms(s.kev[2], s.kev[3]);
+            ++cycles;
             if (s.h_ctl->infeasible) {
                 status = KS_E_INFEASIBLE;
                 break;
             }
-            int did = 0;
-            for (int k = 0; k < K; ++k) did += s.h_ctl->active[k] ? 1 : 0;
-            phase_sweeps += did;
-            if (!s.h_ctl->active[K - 1]) break;
-            since_gu += K;
-            if (since_gu >= gu_interval) {
-                ptrace.back().gu_at.push_back(sweep_launches);
-                KS_CHECK(hipEventRecord(s.ev[6], st));
-                rc = global_update();
-                if (rc) return rc;
-                KS_CHECK(hipEventRecord(s.ev[7], st));
-                KS_CHECK(hipEventSynchronize(s.ev[7]));
-                ms_gu += ev_ms(s.ev[6], s.ev[7]);
-                since_gu = 0;
-                KS_CHECK(read_ctl());
-                if (s.h_ctl->infeasible) {
-                    status = KS_E_INFEASIBLE;
-                    break;
-                }
+            if (!s.h_ctl->bf_done) {
+                // update still running: sweeps were skipped, keep relaxing
+                gu_running = true;
+                kb = std::min(256, kb * 2);
+                sseq += gi;
+                continue;
             }
-            const double wall_s =
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count();
-            if (phase_sweeps > (uint64_t)(64 * (n + 64)) || wall_s > kSolveWallLimitS) {
+            gu_running = false;
+            kb = std::max(8, std::min(256, s.h_ctl->bf_count - gu_r0 + 6));
+            ++gus;
+            sweeps += gi;
+            sweep_launches += gi;
+            sseq += gi;
+            phase_sweeps += gi;
+            int last = 0;
+            for (int k = 0; k < gi; ++k)
+                if (s.h_ctl->sweep_act[k]) last = k + 1;
+            if (!s.h_ctl->sweep_act[gi - 1]) {
+                sweeps -= gi - last;
+                break;   // no excess left: refine done
+            }
+            if (phase_sweeps > (uint64_t)(64 * (n + 64)) || wall_s() > kSolveWallLimitS) {
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
-                      std::to_string(wall_s) + " s)";
+                      std::to_string(wall_s()) + " s)";
                 return KS_E_DEVICE;
             }
         }
@@ -1321,25 +1533,30 @@ int Engine::solve(ks_result& res, std::string& err) {
         KS_CHECK(hipEventSynchronize(s.ev[5]));
         ptrace.back().end = sweep_launches;
         ms_sat += ev_ms(s.ev[2], s.ev[3]);
-        ms_gu += ev_ms(s.ev[3], s.ev[4]);
-        ms_sweep += ev_ms(s.ev[4], s.ev[5]);
-        sweeps += phase_sweeps;
+        ms_cycles += ev_ms(s.ev[3], s.ev[5]);
         if (status) break;
-        if (s.h_ctl->infeasible) {
-            status = KS_E_INFEASIBLE;
-            break;
+        // certify optimality early: a flow that is 1-optimal (scaled) is optimal.
+        // Tried once ε is below 1/32 of a cost unit, where it usually succeeds.
+        if (use_pr && eps > 1 && eps * 32 < mult) {
+            int used = 0;
+            int rc = price_refine(1, &used);
+            if (rc < 0) return rc;
+            if (rc == 1) {
+                ++pr_skips;
+                eps = 1;
+                ptrace.push_back(PhaseRec{1, sweep_launches, sweep_launches, {}, used});
+            }
         }
     } while (eps > 1);
 
-    if (status == KS_E_INFEASIBLE) {
-        err = "infeasible: some supply cannot reach a demand node";
-    }
+    if (status == KS_E_INFEASIBLE) err = "infeasible: some supply cannot reach a demand node";
 
     // ------------------------------------------------------------ verify ---
     KS_CHECK(hipEventRecord(s.ev[6], st));
     const int vgrid = grid_for(m, 2048);
     long long tot_cost = 0;
     if (status == KS_OK) {
+        KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
         if (m) {
             hipLaunchKernelGGL(k_verify_arcs, dim3(vgrid), dim3(BLK), 0, st, g, (const int*)s.fwd.p,
@@ -1367,15 +1584,16 @@ int Engine::solve(ks_result& res, std::string& err) {
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
 
-    if (trace_path && *trace_path && s.trace.n) {
+    if (trace_path && *trace_path && s.trace.n > 1) {
         const uint64_t nt = std::min<uint64_t>(sweep_launches, kTraceMax);
         std::vector<unsigned> ht(4 * nt);
         if (nt) KS_CHECK(hipMemcpy(ht.data(), s.trace.p, 4 * nt * sizeof(unsigned), hipMemcpyDeviceToHost));
         if (FILE* f = std::fopen(trace_path, "a")) {
             std::fprintf(f, "{\"n\": %lld, \"m\": %lld, \"phases\": [", (long long)n, (long long)m);
             for (size_t i = 0; i < ptrace.size(); ++i) {
-                std::fprintf(f, "%s{\"eps\": %lld, \"begin\": %llu, \"end\": %llu, \"gu_at\": [", i ? ", " : "",
-                             ptrace[i].eps, (unsigned long long)ptrace[i].begin, (unsigned long long)ptrace[i].end);
+                std::fprintf(f, "%s{\"eps\": %lld, \"begin\": %llu, \"end\": %llu, \"pr_rounds\": %d, \"gu_at\": [",
+                             i ? ", " : "", ptrace[i].eps, (unsigned long long)ptrace[i].begin,
+                             (unsigned long long)ptrace[i].end, ptrace[i].pr_rounds);
                 for (size_t k = 0; k < ptrace[i].gu_at.size(); ++k)
                     std::fprintf(f, "%s%llu", k ? ", " : "", (unsigned long long)ptrace[i].gu_at[k]);
                 std::fprintf(f, "]}");
@@ -1398,20 +1616,21 @@ int Engine::solve(ks_result& res, std::string& err) {
     res.pushes = tc[C_PUSH];
     res.relabels = tc[C_RELABEL];
     res.global_updates = gus;
-    res.gu_iterations = gu_iters;
+    res.gu_iterations = tc[C_BFROUND];
     res.ms_phase[0] = ev_ms(s.ev[0], s.ev[1]);
     res.ms_phase[1] = ms_sat;
-    res.ms_phase[2] = ms_sweep;
-    res.ms_phase[3] = ms_gu;
+    res.ms_phase[2] = ms_cycles;
+    res.ms_phase[3] = ms_pr;
     res.ms_phase[4] = ev_ms(s.ev[6], s.ev[7]);
-    res.ms_phase[5] =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    res.ms_phase[5] = 1e3 * wall_s();
     res.gu_arc_scans = tc[C_GUSCAN];
     res.sweep_launches = sweep_launches;
-    res.ms_sweep_kernels = ms_sweep_k;
-    res.gu_launches = gu_launches;
-    res.ms_gu_kernels = ms_gu_k;
+    res.ms_sweep_kernels = ms_cycles;
+    res.gu_launches = bf_launches;
+    res.ms_gu_kernels = ms_pr;
     res.status = status;
+    (void)pr_skips;
+    (void)cycles;
     if (status == KS_OK) s.solved = true;
     return status;
 }

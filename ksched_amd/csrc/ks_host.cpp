@@ -254,8 +254,8 @@ void ks_default_opts(ks_opts* o) {
     o->alpha = 16;
     o->verify = 1;
     o->auto_sink = 1;
-    o->sweeps_per_batch = 32;
-    o->gu_interval = 48;
+    o->price_refine = 1;
+    o->gu_interval = 8;
 }
 
 ks_ctx* ks_create(int device, const ks_opts* opts) {

@@ -35,7 +35,7 @@ FLOW_DT = np.dtype({"names": ["src", "dst", "flow"], "formats": ["<u8", "<u8", "
 
 class KsOpts(C.Structure):
     _fields_ = [("alpha", C.c_int32), ("verify", C.c_int32), ("auto_sink", C.c_int32),
-                ("sweeps_per_batch", C.c_int32), ("gu_interval", C.c_int32), ("reserved", C.c_int32 * 11)]
+                ("price_refine", C.c_int32), ("gu_interval", C.c_int32), ("reserved", C.c_int32 * 11)]
 
 
 class KsResult(C.Structure):

@@ -35,7 +35,7 @@ def test_abi_version_and_default_opts():
     assert lib.ks_abi_version() == 1
     o = native.default_opts()
     assert (o.alpha, o.verify, o.auto_sink) == (16, 1, 1)
-    assert o.sweeps_per_batch > 0 and o.gu_interval > 0
+    assert o.price_refine == 1 and o.gu_interval > 0
 
 
 def test_create_fails_loudly_without_device():

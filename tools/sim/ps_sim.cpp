@@ -25,7 +25,7 @@ struct G {
 static i64 floordiv(i64 a, i64 b) { i64 q = a / b; if ((a % b) && (a < 0)) --q; return q; }
 
 struct Opt {
-    int alpha = 16, gi = 48, precise = 0, early_gu = 0, verbose = 1, sat_eps = 0, pref = 0;
+    int alpha = 16, gi = 48, precise = 0, early_gu = 0, verbose = 1, sat_eps = 0, pref = 0, bfk = 0;
 };
 
 struct Stats { i64 sweeps = 0, gus = 0, bf_rounds = 0, visits = 0, relabels = 0, gu_scans = 0, gu_settled = 0; };
@@ -102,6 +102,50 @@ static int price_refine(G& g, i64 eps, int max_rounds, Stats& st) {
     return -1;
 }
 
+// GU by synchronous Bellman-Ford rounds from the deficits, truncated after kmax
+// rounds: d' = min(d, L), L = min distance still on the frontier (valid cap).
+static void gu_bf(G& g, i64 eps, int kmax, Stats& st) {
+    const int n = g.n;
+    std::vector<i64> d(n, INF);
+    std::vector<char> fr(n, 0), nf(n, 0);
+    for (int v = 0; v < n; ++v) if (g.excess[v] < 0) { d[v] = 0; fr[v] = 1; }
+    int rounds = 0;
+    bool any = true;
+    while (any && rounds < kmax) {
+        any = false;
+        std::vector<i64> dn = d;
+        for (int v = 0; v < n; ++v) {
+            if (!fr[v]) continue;
+            for (int a = g.first[v]; a < g.first[v + 1]; ++a) {
+                int ra = g.rev[a];
+                if (g.rcap[ra] <= 0) continue;
+                int u = g.head[a];
+                i64 rc = g.cost[ra] + g.P[u] - g.P[v];
+                i64 nd = d[v] + std::max<i64>(0, floordiv(rc, eps) + 1);
+                if (nd < dn[u]) { dn[u] = nd; nf[u] = 1; any = true; }
+            }
+        }
+        d.swap(dn);
+        fr.swap(nf);
+        std::fill(nf.begin(), nf.end(), 0);
+        rounds++;
+    }
+    i64 L = 0;
+    if (any) {
+        L = INF;
+        for (int v = 0; v < n; ++v) if (fr[v]) L = std::min(L, d[v]);
+    } else {
+        for (int v = 0; v < n; ++v) if (d[v] < INF) L = std::max(L, d[v]);
+    }
+    for (int v = 0; v < n; ++v) {
+        i64 dd = std::min(d[v], L);
+        g.P[v] -= eps * dd;
+        g.PN[v] = g.P[v];
+    }
+    st.gus++;
+    st.bf_rounds += rounds;
+}
+
 int main(int argc, char** argv) {
     i64 T = 100000, M = 10000, R = 250, J = 1000; uint64_t seed = 3;
     Opt o;
@@ -114,6 +158,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "-q")) o.verbose = 0;
         else if (!strcmp(argv[i], "-s")) o.sat_eps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-r")) o.pref = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-k")) o.bfk = atoi(argv[++i]);
     }
     int64_t n, m;
     ko_quincy_sizes(T, M, R, J, &n, &m);
@@ -160,7 +205,7 @@ int main(int argc, char** argv) {
                     i64 r = g.rcap[a]; g.rcap[a] = 0; g.rcap[g.rev[a]] += r;
                     g.excess[u] -= r; g.excess[g.head[a]] += r;
                 }
-        gu(g, eps, o.early_gu, ph);
+        if (o.bfk) gu_bf(g, eps, o.bfk, ph); else gu(g, eps, o.early_gu, ph);
         int since = 0;
         for (;;) {
             int nact = 0;
@@ -203,7 +248,7 @@ int main(int argc, char** argv) {
                 }
             }
             for (int v = 0; v < n; ++v) g.P[v] = g.PN[v];
-            if (++since >= o.gi) { gu(g, eps, o.early_gu, ph); since = 0; }
+            if (++since >= o.gi) { if (o.bfk) gu_bf(g, eps, o.bfk, ph); else gu(g, eps, o.early_gu, ph); since = 0; }
             if (ph.sweeps > 2000000) { fprintf(stderr, "no convergence\n"); return 1; }
         }
         if (o.verbose)
