@@ -4,14 +4,15 @@
 // (scheduling/flow/placement/solver.go:30-34, 60-90). Algorithm and data
 // layout: DESIGN.md §3-§4. Summary:
 //
-//   build      residual CSR from the device-resident input arcs: a stable radix
-//              sort of the 2m (tail, slot) keys (hipcub over rocPRIM), lower
-//              bounds transformed into node excess. Nodes are classed by degree
-//              into lane GROUPS of 4/8/16/32/64 lanes per node (one residual arc
-//              per lane: a node costs one short dependent chain, not a serial
-//              arc loop) plus heavy hubs (1024-arc chunks, one workgroup per
-//              chunk). An ORDER array lists the nodes class by class, each class
-//              padded to 64 slots, so a 64-slot window is single-class.
+//   build      Nodes are RENUMBERED internally: classed by residual degree into
+//              lane GROUPS of 4/8/16/32/64 lanes per node (one residual arc per
+//              lane: a node costs one short dependent chain, not a serial arc
+//              loop), each class a contiguous id range padded to whole 64-node
+//              blocks, heavy hubs (degree > 4096; cluster aggregator, sink) last.
+//              The residual CSR over the new ids comes from a radix sort of the
+//              2m (tail, slot) keys (hipcub over rocPRIM). Every arc also keeps
+//              its pair capacity ucap = rcap(a) + rcap(rev a), so the reverse
+//              residual is ucap − rcap (no gather) and a push is two stores.
 //   phases     ε ← ε/α: saturate every residual arc with negative reduced cost,
 //              then alternate a GLOBAL PRICE UPDATE (Bellman-Ford from the
 //              deficits) with a short burst of push/relabel SWEEPS until no node
@@ -20,12 +21,11 @@
 //              difference constraints of 1-optimality); success proves the flow
 //              optimal and ends the solve early.
 //   frontier   sweeps and Bellman-Ford rounds only touch the ACTIVE frontier:
-//              one flag byte per order slot (three rotating buffers) plus
-//              per-hub flags. Producers store 1 (idempotent, no counters, no
-//              returning atomics); the consumer ballots 64 flags per wave,
-//              clears what it reads and hands active nodes to its lane groups.
-//              Dense passes (saturate, the first round of an update) map every
-//              group to one node statically instead.
+//              one flag byte per node (three rotating buffers) plus per-hub
+//              flags. Producers store 1 (idempotent: no counters, no returning
+//              atomics); a wave owns a window of one or two lane-group batches,
+//              ballots its flags, clears what it reads and hands the active
+//              nodes to its groups. Dense passes take every node.
 //   sweep      every frontier node discharges once against a price SNAPSHOT
 //              (double-buffered prices: read P[q], write P[q^1]); a node
 //              relabels only if it saturated all of its own admissible arcs, and
@@ -36,10 +36,10 @@
 //              [k Bellman-Ford rounds] [max] [apply] [g sweeps]; kernels read
 //              device-side flags and exit early once their stage is finished,
 //              so a cycle costs one host synchronisation.
-//   heavy hubs pushes into a hub (cluster aggregator, sink) are wave-aggregated
-//              into a 16-way sharded inbox; hub chunks claim excess with a CAS
-//              and the last-arriving chunk finalises the relabel. Bellman-Ford
-//              relaxations into a hub are min-reduced in LDS per workgroup.
+//   heavy hubs pushes into a hub are wave-aggregated into a 16-way sharded
+//              inbox; hub chunks claim excess with a CAS and the last-arriving
+//              chunk finalises the relabel. Bellman-Ford relaxations into a hub
+//              are min-reduced in LDS per workgroup.
 //   verify     on-device: conservation, capacity, and 1-optimality of the final
 //              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
 //              the total cost is reduced in int64.
@@ -66,8 +66,7 @@ constexpr int WAVE = 64;
 constexpr int WPB = BLK / WAVE;
 constexpr int NGC = 5;             // group classes: 4, 8, 16, 32, 64 lanes per node
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
-constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
-constexpr int PER_T = CHUNK / BLK;
+constexpr int CHUNK = 256;         // heavy hubs: one residual arc per thread
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -100,35 +99,37 @@ __host__ __device__ constexpr int class_lanes(int c) { return c < 4 ? (4 << c) :
 __host__ __device__ inline int degree_class(int d) {
     return d <= 4 ? 0 : d <= 8 ? 1 : d <= 16 ? 2 : d <= 32 ? 3 : d <= HEAVY_MIN ? 4 : NGC;
 }
+// A wave owns one window: win_batches(c) batches of 64/G consecutive node ids.
+__host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
+__host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
 
-// One frontier buffer: a flag byte per order slot, a flag per hub.
+// One frontier buffer: a flag byte per (non-hub) node, a flag per hub.
 struct Front {
-    unsigned char* flag;   // [n_pad]
+    unsigned char* flag;   // [hub_base]
     int* hub;              // [nheavy]
 };
 
 struct DG {
-    int n, m;
+    int n;                 // internal node ids: [0, hub_base) grouped nodes, then hubs
+    int m;
+    int hub_base;
     const int* first;
     const int* head;
     const int* rev;
     long long* rcap;
+    const long long* ucap;   // rcap(a) + rcap(rev a), constant
     const long long* cost;
     long long* excess;
     long long* p0;
     long long* p1;
     long long* dist;
-    const int* hidx;
     long long* inbox;
-    const int* order;      // [n_pad] nodes class by class, −1 padding
-    const int* fidx;       // [n] node → order slot (−1 for hubs)
-    int n_pad;
-    int wbeg[NGC + 1];     // windows (one per wave) of class c: [wbeg[c], wbeg[c+1])
-    int obeg[NGC + 1];     // first order slot of class c
+    int wbeg[NGC + 1];     // windows of class c: [wbeg[c], wbeg[c+1])
+    int obeg[NGC + 1];     // first node id of class c
+    int oend[NGC];         // one past the last real node of class c
     const HItem* hitems;
     int nhitems;
     int nheavy;
-    const int* hnode;
     const int* hnchunks;
     int* harrive;
     long long* hmin;
@@ -220,9 +221,8 @@ __device__ __forceinline__ long long floordiv(long long a, long long b) {  // b 
 
 // Mark node w active in frontier f (idempotent plain stores).
 __device__ __forceinline__ void mark(const DG& g, const Front& f, int w, int& out) {
-    const int h = g.hidx[w];
-    if (h >= 0) f.hub[h] = 1;
-    else f.flag[g.fidx[w]] = 1;
+    if (w >= g.hub_base) f.hub[w - g.hub_base] = 1;
+    else f.flag[w] = 1;
     out = 1;
 }
 
@@ -249,22 +249,23 @@ __device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
     }
 }
 
-// Push d units of excess into node w (fire-and-forget atomics) and mark w in
-// the next frontier (nf may be null: the saturate pass tracks nothing).
-__device__ __forceinline__ void push_excess(const DG& g, const Front* nf, int w, long long d, Pend& pd, int& out) {
-    const int h = g.hidx[w];
-    if (h < 0) {
+// Push d units along arc a (v → w): residuals are two plain stores (only v's
+// discharge writes the pair this sweep), the excess a fire-and-forget atomic.
+// Non-hub heads are marked in nf (when given); hub pushes are buffered in pd
+// and flagged once per wave in flush_pending.
+__device__ __forceinline__ void push_arc(const DG& g, const Front* nf, int a, int w, long long r, long long d,
+                                         Pend& pd, int& out) {
+    g.rcap[a] = r - d;
+    g.rcap[g.rev[a]] = g.ucap[a] - (r - d);
+    if (w < g.hub_base) {
         atom_add(&g.excess[w], d);
         if (nf) {
-            nf->flag[g.fidx[w]] = 1;
+            nf->flag[w] = 1;
             out = 1;
         }
         return;
     }
-    if (nf) {
-        nf->hub[h] = 1;
-        out = 1;
-    }
+    const int h = w - g.hub_base;
     if (pd.key == h) {
         pd.val += d;
     } else if (pd.key < 0) {
@@ -272,11 +273,15 @@ __device__ __forceinline__ void push_excess(const DG& g, const Front* nf, int w,
         pd.val = d;
     } else {
         atom_add(&g.inbox[h * SHARDS + (blockIdx.x & (SHARDS - 1))], d);
+        if (nf) {
+            nf->hub[h] = 1;
+            out = 1;
+        }
     }
 }
 
 // Must be called by all 64 lanes of a wave at a converged point.
-__device__ __forceinline__ void flush_pending(const DG& g, Pend& pd) {
+__device__ __forceinline__ void flush_pending(const DG& g, const Front* nf, Pend& pd, int& out) {
     const int lane = lane_id();
     for (;;) {
         const unsigned long long msk = __ballot(pd.key >= 0);
@@ -284,17 +289,23 @@ __device__ __forceinline__ void flush_pending(const DG& g, Pend& pd) {
         const int leader = __ffsll((long long)msk) - 1;
         const int k = __shfl(pd.key, leader);
         const long long s = wave_sum(pd.key == k ? pd.val : 0);
-        if (lane == leader) atom_add(&g.inbox[k * SHARDS + (blockIdx.x & (SHARDS - 1))], s);
+        if (lane == leader) {
+            atom_add(&g.inbox[k * SHARDS + (blockIdx.x & (SHARDS - 1))], s);
+            if (nf) {
+                nf->hub[k] = 1;
+                out = 1;
+            }
+        }
         if (pd.key == k) pd.key = -1;
     }
 }
 
 // Drain a hub's inbox shards into its excess. Returns the drained amount.
-__device__ __forceinline__ long long drain_inbox(const DG& g, int h, int x) {
+__device__ __forceinline__ long long drain_inbox(const DG& g, int h) {
     long long s = 0;
 #pragma unroll
     for (int k = 0; k < SHARDS; ++k) s += atom_exch(&g.inbox[h * SHARDS + k], 0LL);
-    if (s) atom_add(&g.excess[x], s);
+    if (s) atom_add(&g.excess[g.hub_base + h], s);
     return s;
 }
 
@@ -339,13 +350,10 @@ __device__ __forceinline__ long long block_excl_scan(long long x, long long* sh,
 }
 
 // --------------------------------------------------- frontier traversal ---
-// A wave owns one WINDOW of class C: win_batches(C) batches of 64/G order slots.
-// It ballots the window's flags (clearing what it reads; dense passes take every
-// real node), then hands the active nodes to its G-lane groups one batch at a
-// time. The loop trip count is wave-uniform, so CALL may use wave collectives.
-__host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
-__host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
-
+// A wave owns one window of class C. It ballots the window's flags (clearing
+// what it reads; dense passes take every real node) and hands the active nodes
+// to its G-lane groups one batch at a time. The loop trip count is wave-uniform,
+// so the group code may use wave collectives.
 #define KS_WINDOW(C, ARGS, W, ...)                                                   \
     {                                                                                \
         constexpr int G_ = class_lanes(C);                                           \
@@ -356,7 +364,7 @@ __host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64
         bool on_ = false;                                                            \
         if (ln_ < WS_) {                                                             \
             if ((ARGS).dense) {                                                      \
-                on_ = g.order[base_ + ln_] >= 0;                                     \
+                on_ = base_ + ln_ < g.oend[C];                                       \
             } else {                                                                 \
                 on_ = (ARGS).flags[base_ + ln_] != 0;                                \
                 if (on_) (ARGS).flags[base_ + ln_] = 0;                              \
@@ -367,7 +375,7 @@ __host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64
         while (mask_) {                                                              \
             unsigned long long mm_ = mask_;                                          \
             for (int j_ = 0; j_ < k_; ++j_) mm_ &= mm_ - 1;                          \
-            const int v = mm_ ? g.order[base_ + __ffsll((long long)mm_) - 1] : -1;   \
+            const int v = mm_ ? base_ + __ffsll((long long)mm_) - 1 : -1;            \
             __VA_ARGS__;                                                             \
             for (int j_ = 0; j_ < PER_; ++j_) mask_ &= mask_ - 1;                    \
         }                                                                            \
@@ -393,12 +401,15 @@ __device__ __forceinline__ int wave_index_in_grid(int first_block) {
 
 // ===================================================================== build ===
 __global__ void k_make_keys(int m, const int* __restrict__ src, const int* __restrict__ dst,
-                            unsigned* __restrict__ keys, int* __restrict__ vals) {
+                            const int* __restrict__ perm, unsigned* __restrict__ keys, int* __restrict__ vals) {
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
-        keys[2 * i] = (unsigned)src[i];
-        keys[2 * i + 1] = (unsigned)dst[i];
-        vals[2 * i] = (int)(2 * i);
-        vals[2 * i + 1] = (int)(2 * i + 1);
+        const int s = src[i], d = dst[i];
+        keys[2 * i] = (unsigned)(perm ? perm[s] : s);
+        keys[2 * i + 1] = (unsigned)(perm ? perm[d] : d);
+        if (vals) {
+            vals[2 * i] = (int)(2 * i);
+            vals[2 * i + 1] = (int)(2 * i + 1);
+        }
     }
 }
 
@@ -408,24 +419,28 @@ __global__ void k_scatter_pos(long long m2, const int* __restrict__ vals, int* _
 }
 
 __global__ void k_fill(long long m2, long long mult, const int* __restrict__ vals, const int* __restrict__ pos_of,
-                       const int* __restrict__ src, const int* __restrict__ dst, const long long* __restrict__ low,
-                       const long long* __restrict__ cap, const long long* __restrict__ cost, int* __restrict__ head,
-                       int* __restrict__ rev, long long* __restrict__ rcap, long long* __restrict__ scost,
+                       const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
+                       const long long* __restrict__ low, const long long* __restrict__ cap,
+                       const long long* __restrict__ cost, int* __restrict__ head, int* __restrict__ rev,
+                       long long* __restrict__ rcap, long long* __restrict__ ucap, long long* __restrict__ scost,
                        int* __restrict__ fwd) {
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
         const int v = vals[p];
         const int i = v >> 1;
         const bool r = v & 1;
-        head[p] = r ? src[i] : dst[i];
+        head[p] = perm[r ? src[i] : dst[i]];
         rev[p] = pos_of[v ^ 1];
-        rcap[p] = r ? 0 : cap[i] - low[i];
+        const long long u = cap[i] - low[i];
+        rcap[p] = r ? 0 : u;
+        ucap[p] = u;
         scost[p] = (r ? -cost[i] : cost[i]) * mult;
         if (!r) fwd[i] = (int)p;
     }
 }
 
-__global__ void k_first(int n, long long m2, const unsigned* __restrict__ keys, int* __restrict__ first) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v <= n; v += (long long)gridDim.x * BLK) {
+// first[v] = lower bound of v in the sorted keys, v ∈ [0, nn].
+__global__ void k_first(int nn, long long m2, const unsigned* __restrict__ keys, int* __restrict__ first) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v <= nn; v += (long long)gridDim.x * BLK) {
         long long lo = 0, hi = m2;
         while (lo < hi) {
             const long long mid = (lo + hi) >> 1;
@@ -435,42 +450,42 @@ __global__ void k_first(int n, long long m2, const unsigned* __restrict__ keys, 
     }
 }
 
-__global__ void k_node_init(int n, const long long* __restrict__ supply, const int* __restrict__ first,
-                            long long* __restrict__ excess, long long* __restrict__ p0, long long* __restrict__ p1,
-                            unsigned char* __restrict__ cls, int* __restrict__ hidx, int* __restrict__ fidx) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
-        excess[v] = supply[v];
+__global__ void k_classify(int n, const int* __restrict__ first, unsigned char* __restrict__ cls) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
+        cls[v] = (unsigned char)degree_class(first[v + 1] - first[v]);
+}
+
+// perm[list[i]] = base + i (one class, or the hubs).
+__global__ void k_make_perm(int cnt, int base, const int* __restrict__ list, int* __restrict__ perm) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < cnt; i += (long long)gridDim.x * BLK)
+        perm[list[i]] = base + (int)i;
+}
+
+__global__ void k_node_init(int nn, long long* __restrict__ excess, long long* __restrict__ p0,
+                            long long* __restrict__ p1) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < nn; v += (long long)gridDim.x * BLK) {
+        excess[v] = 0;
         p0[v] = 0;
         p1[v] = 0;
-        cls[v] = (unsigned char)degree_class(first[v + 1] - first[v]);
-        hidx[v] = -1;
-        fidx[v] = -1;
     }
+}
+
+// excess[perm[v]] = supply[v]; then the lower-bound transform per arc.
+__global__ void k_supply(int n, const long long* __restrict__ supply, const int* __restrict__ perm,
+                         long long* __restrict__ excess) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
+        excess[perm[v]] = supply[v];
 }
 
 __global__ void k_lower_bounds(int m, const int* __restrict__ src, const int* __restrict__ dst,
-                               const long long* __restrict__ low, long long* __restrict__ excess) {
+                               const int* __restrict__ perm, const long long* __restrict__ low,
+                               long long* __restrict__ excess) {
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
         const long long l = low[i];
         if (l) {
-            atom_add(&excess[src[i]], -l);
-            atom_add(&excess[dst[i]], l);
+            atom_add(&excess[perm[src[i]]], -l);
+            atom_add(&excess[perm[dst[i]]], l);
         }
-    }
-}
-
-__global__ void k_set_hidx(int nheavy, const int* __restrict__ hnode, int* __restrict__ hidx) {
-    const int h = blockIdx.x * BLK + threadIdx.x;
-    if (h < nheavy) hidx[hnode[h]] = h;
-}
-
-// order[obeg + i] = list[i], fidx[list[i]] = obeg + i (one class).
-__global__ void k_make_order(int cnt, int obeg, const int* __restrict__ list, int* __restrict__ order,
-                             int* __restrict__ fidx) {
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < cnt; i += (long long)gridDim.x * BLK) {
-        const int v = list[i];
-        order[obeg + i] = v;
-        fidx[v] = obeg + (int)i;
     }
 }
 
@@ -503,15 +518,13 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, Pend& pd, int& out
             if (r > 0) {
                 const int w = g.head[a];
                 if (g.cost[a] + pv - P[w] < 0) {
-                    g.rcap[a] = 0;
-                    g.rcap[g.rev[a]] += r;
-                    push_excess(g, nullptr, w, r, pd, out);
+                    push_arc(g, nullptr, a, w, r, r, pd, out);
                     tot += r;
                     c.push++;
                 }
             }
         }
-        flush_pending(g, pd);
+        flush_pending(g, nullptr, pd, out);
     }
     tot = g_sum<G>(tot);
     if (v >= 0 && lig == 0 && tot) atom_add(&g.excess[v], -tot);
@@ -527,23 +540,19 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
         const HItem it = g.hitems[blockIdx.x];
         const long long px = P[it.node];
         long long tot = 0;
-        for (int k = 0; k < PER_T; ++k) {
-            const int a = it.begin + threadIdx.x + k * BLK;
-            if (a < it.end) {
-                const long long r = g.rcap[a];
-                if (r > 0) {
-                    const int w = g.head[a];
-                    if (g.cost[a] + px - P[w] < 0) {
-                        g.rcap[a] = 0;
-                        g.rcap[g.rev[a]] += r;
-                        push_excess(g, nullptr, w, r, pd, out);
-                        tot += r;
-                        c.push++;
-                    }
+        const int a = it.begin + threadIdx.x;
+        if (a < it.end) {
+            const long long r = g.rcap[a];
+            if (r > 0) {
+                const int w = g.head[a];
+                if (g.cost[a] + px - P[w] < 0) {
+                    push_arc(g, nullptr, a, w, r, r, pd, out);
+                    tot += r;
+                    c.push++;
                 }
             }
         }
-        flush_pending(g, pd);
+        flush_pending(g, nullptr, pd, out);
         tot = block_sum(tot, sh);
         if (threadIdx.x == 0 && tot) atom_add(&g.excess[it.node], -tot);
         flush_counters(g, c);
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
 #define KS_SAT_CALL(C) sat_group<G_>(g, v, pd, out, c)
     KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SAT_CALL)
 #undef KS_SAT_CALL
-    flush_pending(g, pd);
+    flush_pending(g, nullptr, pd, out);
     flush_counters(g, c);
 }
 
@@ -594,9 +603,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         long long d = rem - (incl - adm);
         d = d < 0 ? 0 : (d > adm ? adm : d);
         if (d > 0) {
-            g.rcap[a] = r - d;
-            g.rcap[g.rev[a]] += d;
-            push_excess(g, &nf, w, d, pd, out);
+            push_arc(g, &nf, a, w, r, d, pd, out);
             c.push++;
         }
         if (valid) {
@@ -607,7 +614,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
             }
         }
         rem -= total < rem ? total : rem;
-        flush_pending(g, pd);
+        flush_pending(g, &nf, pd, out);
         if (G == 64 && rem == 0) break;
     }
     minc = g_min<G>(minc);
@@ -619,7 +626,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
             if (minc >= INF64) g.ctl->infeasible = 1;
             else np = pv - (minc + eps);
             c.relabel++;
-            nf.flag[g.fidx[v]] = 1;   // still active next sweep
+            nf.flag[v] = 1;   // still active next sweep
             out = 1;
         }
         PN[v] = np;
@@ -644,54 +651,38 @@ __device__ void heavy_chunk(const DG& g, const Front& nf, const HItem& it, const
     __shared__ long long s_take;
     const int x = it.node, h = it.hid;
     const bool chunk0 = it.begin == g.first[x];
-    if (chunk0 && threadIdx.x == 0) drain_inbox(g, h, x);
+    if (chunk0 && threadIdx.x == 0) drain_inbox(g, h);
     const long long px = P[x];
-    long long r[PER_T], cr[PER_T], adm[PER_T];
-    int w[PER_T];
-    long long mine = 0;
-#pragma unroll
-    for (int k = 0; k < PER_T; ++k) {
-        const int a = it.begin + threadIdx.x * PER_T + k;
-        r[k] = 0;
-        cr[k] = 0;
-        w[k] = 0;
-        if (a < it.end) {
-            r[k] = g.rcap[a];
-            w[k] = g.head[a];
-            cr[k] = g.cost[a] + px - P[w[k]];
-            c.scan++;
-        }
-        adm[k] = (a < it.end && cr[k] < 0 && r[k] > 0) ? r[k] : 0;
-        mine += adm[k];
+    const int a = it.begin + threadIdx.x;
+    long long r = 0, cr = 0;
+    int w = 0;
+    if (a < it.end) {
+        r = g.rcap[a];
+        w = g.head[a];
+        cr = g.cost[a] + px - P[w];
+        c.scan++;
     }
+    const long long adm = (a < it.end && cr < 0 && r > 0) ? r : 0;
     long long Ac = 0;
-    const long long excl = block_excl_scan(mine, sh, &Ac);
+    const long long excl = block_excl_scan(adm, sh, &Ac);
     if (threadIdx.x == 0) s_take = heavy_claim(&g.excess[x], Ac);
     __syncthreads();
     const long long take = s_take;
-    long long rt = take - excl;
-    rt = rt < 0 ? 0 : (rt > mine ? mine : rt);
+    long long d = take - excl;
+    d = d < 0 ? 0 : (d > adm ? adm : d);
+    if (d > 0) {
+        push_arc(g, &nf, a, w, r, d, pd, out);
+        c.push++;
+    }
     long long minc = INF64;
-#pragma unroll
-    for (int k = 0; k < PER_T; ++k) {
-        const int a = it.begin + threadIdx.x * PER_T + k;
-        long long d = adm[k] < rt ? adm[k] : rt;
-        rt -= d;
-        if (d > 0) {
-            g.rcap[a] = r[k] - d;
-            g.rcap[g.rev[a]] += d;
-            push_excess(g, &nf, w[k], d, pd, out);
-            c.push++;
-        }
-        if (a < it.end) {
-            if (cr[k] < 0) {
-                if (r[k] - d > 0) minc = min(minc, cr[k]);
-            } else if (r[k] > 0 || cr[k] <= eps) {
-                minc = min(minc, cr[k]);
-            }
+    if (a < it.end) {
+        if (cr < 0) {
+            if (r - d > 0) minc = cr;
+        } else if (r > 0 || cr <= eps) {
+            minc = cr;
         }
     }
-    flush_pending(g, pd);
+    flush_pending(g, &nf, pd, out);
     minc = block_min(minc, sh);
     if (threadIdx.x == 0) {
         if (minc < INF64) atom_min_ret(&g.hmin[h], minc);
@@ -759,29 +750,35 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
 // of length clamp(floor(rc/ε)+1, 0, LEN_CAP), unreached = INF.
 // Price refinement (PR): all distances start at 0, lengths floor(rc/ε)+1 may be
 // negative (difference constraints of ε-optimality).
-// Push-style: a node whose distance dropped relaxes its IN-arcs (u→v), found as
-// the reverses of its CSR arcs (cost(u→v) = −cost(v→u)). No returning atomics:
-// a plain pre-check filters (a stale distance is only larger), atomicMin
-// commits, the flag store marks u for the next round.
+// Push-style: a node whose distance dropped relaxes its IN-arcs (u→v), i.e. the
+// reverses of its CSR arcs a = (v→u): residual ucap(a) − rcap(a), cost −cost(a).
+// No returning atomics: a plain pre-check filters (a stale distance is only
+// larger), atomicMin commits, the flag store marks u for the next round.
 template <bool PR>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
                                          long long eps, long long* hub_min, int& out) {
-    const int ra = g.rev[a];
-    if (g.rcap[ra] <= 0) return;
+    const long long rin = g.ucap[a] - g.rcap[a];
     const int u = g.head[a];
-    const long long cr = -g.cost[a] + g.p0[u] - pv;
-    long long len = floordiv(cr, eps) + 1;
+    const long long ca = g.cost[a];
+    if (rin <= 0) return;
+    const long long pu = g.p0[u];
+    const long long du = u < g.hub_base ? g.dist[u] : INF64;
+    long long len = floordiv(pu - ca - pv, eps) + 1;
     if (!PR) len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
     const long long cand = dv + len;
-    const int h = g.hidx[u];
-    if (h >= 0 && h < HUB_LDS) {
-        __hip_atomic_fetch_min(&hub_min[h], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (u >= g.hub_base) {
+        const int h = u - g.hub_base;
+        if (h < HUB_LDS) {
+            __hip_atomic_fetch_min(&hub_min[h], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (cand < atom_min_ret(&g.dist[u], cand)) {
+            nf.hub[h] = 1;
+            out = 1;
+        }
         return;
     }
-    if (cand >= g.dist[u]) return;
+    if (cand >= du) return;
     atom_min(&g.dist[u], cand);
-    if (h >= 0) nf.hub[h] = 1;
-    else nf.flag[g.fidx[u]] = 1;
+    nf.flag[u] = 1;
     out = 1;
 }
 
@@ -833,13 +830,10 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
         if (dense || F.hub[it.hid]) {
             const long long dv = atom_load(&g.dist[it.node]);
             if (PR || dv < INF64) {
-                const long long pv = g.p0[it.node];
-                for (int k = 0; k < PER_T; ++k) {
-                    const int a = it.begin + threadIdx.x * PER_T + k;
-                    if (a < it.end) {
-                        relax_in<PR>(g, N, a, dv, pv, eps, hub_min, out);
-                        scans++;
-                    }
+                const int a = it.begin + threadIdx.x;
+                if (a < it.end) {
+                    relax_in<PR>(g, N, a, dv, g.p0[it.node], eps, hub_min, out);
+                    scans++;
                 }
             }
         }
@@ -853,8 +847,8 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     if (threadIdx.x < HUB_LDS && (int)threadIdx.x < g.nheavy) {
         const long long val = hub_min[threadIdx.x];
         if (val < INF64) {
-            const long long old = atom_min_ret(&g.dist[g.hnode[threadIdx.x]], val);
-            if (val < old) {
+            long long* dx = &g.dist[g.hub_base + threadIdx.x];
+            if (val < atom_load(dx) && val < atom_min_ret(dx, val)) {
                 N.hub[threadIdx.x] = 1;
                 out = 1;
             }
@@ -873,7 +867,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
 }
 
 __device__ __forceinline__ void clear_fronts(const DG& g, const Front* fs) {
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < g.n_pad; i += (long long)gridDim.x * BLK) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < g.hub_base; i += (long long)gridDim.x * BLK) {
         fs[0].flag[i] = 0;
         fs[1].flag[i] = 0;
         fs[2].flag[i] = 0;
@@ -891,9 +885,13 @@ __global__ void k_gu_init(DG g) {
         g.ctl->bfa[0] = g.ctl->bfa[1] = g.ctl->bfa[2] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const int h = g.hidx[v];
-        if (h >= 0) drain_inbox(g, h, (int)v);
-        const long long e = h >= 0 ? atom_load(&g.excess[v]) : g.excess[v];
+        long long e;
+        if (v >= g.hub_base) {
+            drain_inbox(g, (int)v - g.hub_base);
+            e = atom_load(&g.excess[v]);
+        } else {
+            e = g.excess[v];
+        }
         g.dist[v] = e < 0 ? 0 : INF64;
     }
 }
@@ -972,7 +970,7 @@ __global__ void k_pr_apply(DG g) {
 // Conservation, capacity and 1-optimality (scaled units); per-block cost sums.
 __global__ void k_drain_all(DG g) {
     const int h = blockIdx.x * BLK + threadIdx.x;
-    if (h < g.nheavy) drain_inbox(g, h, g.hnode[h]);
+    if (h < g.nheavy) drain_inbox(g, h);
 }
 
 __global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const long long* __restrict__ low,
@@ -1059,37 +1057,36 @@ struct EngineImpl {
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
 
-    // input (compacted) graph
+    // input (compacted) graph, original ids
     int64_t n = 0, m = 0;
     int64_t maxc = 0;
     DBuf<int> a_src, a_dst;
     DBuf<long long> a_low, a_cap, a_cost, supply;
 
-    // residual CSR and node state
+    // residual CSR and node state, internal ids
     DBuf<unsigned> keys_in, keys_out;
     DBuf<int> vals_in, vals_out, pos_of;
     DBuf<unsigned char> sort_tmp;
-    DBuf<int> first, head, rev, fwd;
-    DBuf<long long> rcap, scost, excess, p0, p1, dist;
-    DBuf<int> order, fidx;
-    DBuf<unsigned char> flags;   // 6 frontier buffers × n_pad
-    DBuf<int> hubflags;          // 6 × nheavy
+    DBuf<int> first, head, rev, fwd, perm;
+    DBuf<long long> rcap, ucap, scost, excess, p0, p1, dist;
     DBuf<unsigned char> cls;
-    DBuf<int> hidx, nsel;
-    DBuf<int> cls_list[NGC + 1];   // every node of each degree class; [NGC] = heavy hubs
+    DBuf<int> nsel;
+    DBuf<int> cls_list[NGC + 1];   // original ids of each degree class; [NGC] = heavy hubs
     DBuf<unsigned char> sel_tmp;
     DBuf<HItem> hitems;
     DBuf<int> hnchunks, harrive, hunsat;
     DBuf<long long> hmin, inbox, part, flows;
+    DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
+    DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
     DBuf<unsigned> trace;
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;       // pinned host mirror
     long long* h_scr = nullptr; // pinned scratch: [0] eps
     int ncls[NGC + 1] = {0};
-    int n_pad = 0;
-    int obeg[NGC + 1] = {0}, wbeg[NGC + 1] = {0};
     int nheavy = 0, nhitems = 0;
+    int hub_base = 0, nn = 0;   // grouped node ids [0, hub_base), hubs after: nn ids
+    int obeg[NGC + 1] = {0}, oend[NGC] = {0}, wbeg[NGC + 1] = {0};
     bool solved = false;
 
     ~EngineImpl() {
@@ -1099,12 +1096,12 @@ struct EngineImpl {
         }
         a_src.release(); a_dst.release(); a_low.release(); a_cap.release(); a_cost.release(); supply.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release();
-        sort_tmp.release(); first.release(); head.release(); rev.release(); fwd.release();
-        rcap.release(); scost.release(); excess.release(); p0.release(); p1.release(); dist.release();
-        order.release(); fidx.release(); flags.release(); hubflags.release(); cls.release(); hidx.release();
+        sort_tmp.release(); first.release(); head.release(); rev.release(); fwd.release(); perm.release();
+        rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release();
+        dist.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
-        nsel.release(); sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release();
-        hunsat.release(); hmin.release(); inbox.release(); part.release(); flows.release();
+        sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release(); hunsat.release();
+        hmin.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
         ctr.release(); trace.release(); ctl.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
@@ -1113,40 +1110,38 @@ struct EngineImpl {
         if (stream) (void)hipStreamDestroy(stream);
     }
 
-
     DG dg() const {
         DG g{};
-        g.n = (int)n;
+        g.n = nn;
         g.m = (int)m;
+        g.hub_base = hub_base;
         g.first = first.p;
         g.head = head.p;
         g.rev = rev.p;
         g.rcap = rcap.p;
+        g.ucap = ucap.p;
         g.cost = scost.p;
         g.excess = excess.p;
         g.p0 = p0.p;
         g.p1 = p1.p;
         g.dist = dist.p;
-        g.order = order.p;
-        g.fidx = fidx.p;
-        g.n_pad = n_pad;
+        g.inbox = inbox.p;
         for (int c = 0; c <= NGC; ++c) {
             g.obeg[c] = obeg[c];
             g.wbeg[c] = wbeg[c];
         }
-        g.hidx = hidx.p;
-        g.inbox = inbox.p;
+        for (int c = 0; c < NGC; ++c) g.oend[c] = oend[c];
         g.hitems = hitems.p;
         g.nhitems = nhitems;
         g.nheavy = nheavy;
-        g.hnode = cls_list[NGC].p;
         g.hnchunks = hnchunks.p;
         g.harrive = harrive.p;
         g.hmin = hmin.p;
         g.hunsat = hunsat.p;
         const int hs = std::max(1, nheavy);
+        const size_t fs = std::max(1, hub_base);
         for (int k = 0; k < 6; ++k) {
-            Front f{flags.p + (size_t)k * n_pad, hubflags.p + (size_t)k * hs};
+            Front f{flags.p + k * fs, hubflags.p + (size_t)k * hs};
             if (k < 3) g.sf[k] = f;
             else g.bf[k - 3] = f;
         }
@@ -1195,7 +1190,7 @@ int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
                    const int64_t* cap, const int64_t* cost, const int64_t* supply, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
-    if (n < 0 || m < 0 || n > (1LL << 29) || m > (1LL << 29)) {
+    if (n < 0 || m < 0 || n > (1LL << 28) || m > (1LL << 29)) {
         err = "graph too large for 32-bit CSR indices";
         return KS_E_RANGE;
     }
@@ -1269,23 +1264,19 @@ int Engine::solve(ks_result& res, std::string& err) {
     KS_CHECK(s.vals_in.ensure(m2));
     KS_CHECK(s.vals_out.ensure(m2));
     KS_CHECK(s.pos_of.ensure(m2));
-    KS_CHECK(s.first.ensure(n + 1));
     KS_CHECK(s.head.ensure(m2));
     KS_CHECK(s.rev.ensure(m2));
     KS_CHECK(s.fwd.ensure(m));
     KS_CHECK(s.rcap.ensure(m2));
+    KS_CHECK(s.ucap.ensure(m2));
     KS_CHECK(s.scost.ensure(m2));
-    KS_CHECK(s.excess.ensure(n));
-    KS_CHECK(s.p0.ensure(n));
-    KS_CHECK(s.p1.ensure(n));
-    KS_CHECK(s.dist.ensure(n));
-    KS_CHECK(s.fidx.ensure(n));
+    KS_CHECK(s.perm.ensure(n));
     KS_CHECK(s.cls.ensure(n));
-    KS_CHECK(s.hidx.ensure(n));
     for (auto& b : s.cls_list) KS_CHECK(b.ensure(n));
     KS_CHECK(s.nsel.ensure(NGC + 1));
     KS_CHECK(s.flows.ensure(m));
     KS_CHECK(s.part.ensure(4096));
+    KS_CHECK(s.first.ensure(n + 2 + 64 * NGC));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
     std::memset(s.h_ctl, 0, sizeof(Ctl));
@@ -1300,34 +1291,30 @@ int Engine::solve(ks_result& res, std::string& err) {
         long long eps;
         uint64_t begin, end;
         std::vector<uint64_t> gu_at;
-        int pr_rounds;   // price-refinement rounds; > 0 success (phase skipped), < 0 failed
+        int pr_rounds;   // price-refinement rounds; > 0 success, < 0 failed
     };
     std::vector<PhaseRec> ptrace;
 
+    int bits = 1;
+    while ((1LL << bits) <= n + 64 * NGC + 1) ++bits;
+    size_t sort_tmp = 0;
+    // 1. degrees in original ids (sorted endpoint keys) → degree classes
     if (m) {
         hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
-                           s.keys_in.p, s.vals_in.p);
-        int bits = 1;
-        while ((1LL << bits) <= n) ++bits;
-        size_t tmp = 0;
-        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, s.keys_in.p, s.keys_out.p, s.vals_in.p,
+                           (const int*)nullptr, s.keys_in.p, (int*)nullptr);
+        KS_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_tmp, s.keys_in.p, s.keys_out.p, (int)m2, 0, bits,
+                                                   st));
+        size_t t2 = 0;
+        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, s.keys_in.p, s.keys_out.p, s.vals_in.p,
                                                     s.vals_out.p, (int)m2, 0, bits, st));
-        KS_CHECK(s.sort_tmp.ensure(tmp));
-        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(s.sort_tmp.p, tmp, s.keys_in.p, s.keys_out.p, s.vals_in.p,
-                                                    s.vals_out.p, (int)m2, 0, bits, st));
-        hipLaunchKernelGGL(k_scatter_pos, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, s.vals_out.p,
-                           s.pos_of.p);
-        hipLaunchKernelGGL(k_fill, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, mult, s.vals_out.p,
-                           s.pos_of.p, s.a_src.p, s.a_dst.p, s.a_low.p, s.a_cap.p, s.a_cost.p, s.head.p, s.rev.p,
-                           s.rcap.p, s.scost.p, s.fwd.p);
+        sort_tmp = std::max(sort_tmp, t2);
+        KS_CHECK(s.sort_tmp.ensure(sort_tmp));
+        KS_CHECK(hipcub::DeviceRadixSort::SortKeys(s.sort_tmp.p, sort_tmp, s.keys_in.p, s.keys_out.p, (int)m2, 0,
+                                                   bits, st));
     }
     hipLaunchKernelGGL(k_first, dim3(grid_for(n + 1)), dim3(BLK), 0, st, (int)n, (long long)m2, s.keys_out.p,
                        s.first.p);
-    hipLaunchKernelGGL(k_node_init, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, s.supply.p, s.first.p,
-                       s.excess.p, s.p0.p, s.p1.p, s.cls.p, s.hidx.p, s.fidx.p);
-    if (m)
-        hipLaunchKernelGGL(k_lower_bounds, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
-                           s.a_low.p, s.excess.p);
+    hipLaunchKernelGGL(k_classify, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const int*)s.first.p, s.cls.p);
     {
         hipcub::CountingInputIterator<int> it(0);
         size_t tmp = 0, t2 = 0;
@@ -1346,22 +1333,66 @@ int Engine::solve(ks_result& res, std::string& err) {
     KS_CHECK(hipMemcpyAsync(s.ncls, s.nsel.p, (NGC + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
     KS_CHECK(hipStreamSynchronize(st));
     s.nheavy = s.ncls[NGC];
+    // 2. internal ids: classes in order, each padded to whole 64-node blocks, hubs last
+    {
+        int o = 0, wv = 0;
+        for (int c = 0; c < NGC; ++c) {
+            s.obeg[c] = o;
+            s.oend[c] = o + s.ncls[c];
+            s.wbeg[c] = wv;
+            const int pad = (s.ncls[c] + 63) / 64 * 64;
+            o += pad;
+            wv += pad / win_slots(c);
+        }
+        s.obeg[NGC] = o;
+        s.wbeg[NGC] = wv;
+        s.hub_base = o;
+        s.nn = o + s.nheavy;
+    }
+    const int nn = s.nn;
+    for (int c = 0; c <= NGC; ++c)
+        if (s.ncls[c])
+            hipLaunchKernelGGL(k_make_perm, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c],
+                               c < NGC ? s.obeg[c] : s.hub_base, (const int*)s.cls_list[c].p, s.perm.p);
+    KS_CHECK(s.excess.ensure(nn));
+    KS_CHECK(s.p0.ensure(nn));
+    KS_CHECK(s.p1.ensure(nn));
+    KS_CHECK(s.dist.ensure(nn));
+    KS_CHECK(s.first.ensure(nn + 1));
+    // 3. residual CSR over internal ids
+    if (m) {
+        hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
+                           (const int*)s.perm.p, s.keys_in.p, s.vals_in.p);
+        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(s.sort_tmp.p, sort_tmp, s.keys_in.p, s.keys_out.p, s.vals_in.p,
+                                                    s.vals_out.p, (int)m2, 0, bits, st));
+        hipLaunchKernelGGL(k_scatter_pos, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, s.vals_out.p,
+                           s.pos_of.p);
+        hipLaunchKernelGGL(k_fill, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, mult, s.vals_out.p,
+                           s.pos_of.p, s.a_src.p, s.a_dst.p, (const int*)s.perm.p, s.a_low.p, s.a_cap.p, s.a_cost.p,
+                           s.head.p, s.rev.p, s.rcap.p, s.ucap.p, s.scost.p, s.fwd.p);
+    }
+    hipLaunchKernelGGL(k_first, dim3(grid_for(nn + 1)), dim3(BLK), 0, st, nn, (long long)m2, s.keys_out.p,
+                       s.first.p);
+    hipLaunchKernelGGL(k_node_init, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, s.excess.p, s.p0.p, s.p1.p);
+    hipLaunchKernelGGL(k_supply, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const long long*)s.supply.p,
+                       (const int*)s.perm.p, s.excess.p);
+    if (m)
+        hipLaunchKernelGGL(k_lower_bounds, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
+                           (const int*)s.perm.p, s.a_low.p, s.excess.p);
     {
         // heavy hubs: chunk table (few hubs; built on host from their CSR ranges)
-        std::vector<int> hn(s.nheavy), hf(2 * s.nheavy);
+        std::vector<int> hf(s.nheavy + 1);
         if (s.nheavy) {
-            KS_CHECK(hipMemcpyAsync(hn.data(), s.cls_list[NGC].p, s.nheavy * sizeof(int), hipMemcpyDeviceToHost, st));
-            KS_CHECK(hipStreamSynchronize(st));
-            for (int h = 0; h < s.nheavy; ++h)
-                KS_CHECK(hipMemcpyAsync(&hf[2 * h], s.first.p + hn[h], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+            KS_CHECK(hipMemcpyAsync(hf.data(), s.first.p + s.hub_base, (s.nheavy + 1) * sizeof(int),
+                                    hipMemcpyDeviceToHost, st));
             KS_CHECK(hipStreamSynchronize(st));
         }
         std::vector<HItem> items;
         std::vector<int> nch(s.nheavy);
         for (int h = 0; h < s.nheavy; ++h) {
             int c = 0;
-            for (int b = hf[2 * h]; b < hf[2 * h + 1]; b += CHUNK, ++c)
-                items.push_back(HItem{hn[h], h, b, std::min(b + CHUNK, hf[2 * h + 1])});
+            for (int b = hf[h]; b < hf[h + 1]; b += CHUNK, ++c)
+                items.push_back(HItem{s.hub_base + h, h, b, std::min(b + CHUNK, hf[h + 1])});
             nch[h] = c;
         }
         s.nhitems = (int)items.size();
@@ -1371,28 +1402,10 @@ int Engine::solve(ks_result& res, std::string& err) {
         KS_CHECK(s.hunsat.ensure(s.nheavy));
         KS_CHECK(s.hmin.ensure(s.nheavy));
         KS_CHECK(s.inbox.ensure((size_t)s.nheavy * SHARDS));
-        // class-ordered slots, each class padded to whole 64-slot windows
-        int o = 0, wv = 0;
-        for (int c = 0; c < NGC; ++c) {
-            s.obeg[c] = o;
-            s.wbeg[c] = wv;
-            const int pad = (s.ncls[c] + 63) / 64 * 64;
-            o += pad;
-            wv += pad / win_slots(c);
-        }
-        s.obeg[NGC] = o;
-        s.wbeg[NGC] = wv;
-        s.n_pad = o;
-        KS_CHECK(s.order.ensure(std::max(1, o)));
-        KS_CHECK(s.flags.ensure(6 * (size_t)std::max(1, o)));
+        KS_CHECK(s.flags.ensure(6 * (size_t)std::max(1, s.hub_base)));
         KS_CHECK(s.hubflags.ensure(6 * (size_t)std::max(1, s.nheavy)));
-        KS_CHECK(hipMemsetAsync(s.order.p, 0xff, std::max(1, o) * sizeof(int), st));
-        KS_CHECK(hipMemsetAsync(s.flags.p, 0, 6 * (size_t)std::max(1, o), st));
+        KS_CHECK(hipMemsetAsync(s.flags.p, 0, 6 * (size_t)std::max(1, s.hub_base), st));
         KS_CHECK(hipMemsetAsync(s.hubflags.p, 0, 6 * (size_t)std::max(1, s.nheavy) * sizeof(int), st));
-        for (int c = 0; c < NGC; ++c)
-            if (s.ncls[c])
-                hipLaunchKernelGGL(k_make_order, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c], s.obeg[c],
-                                   (const int*)s.cls_list[c].p, s.order.p, s.fidx.p);
         if (s.nheavy) {
             std::vector<long long> hm(s.nheavy, INF64);
             KS_CHECK(hipMemcpyAsync(s.hitems.p, items.data(), items.size() * sizeof(HItem), hipMemcpyHostToDevice, st));
@@ -1401,8 +1414,6 @@ int Engine::solve(ks_result& res, std::string& err) {
             KS_CHECK(hipMemsetAsync(s.harrive.p, 0, s.nheavy * sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.hunsat.p, 0, s.nheavy * sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.inbox.p, 0, (size_t)s.nheavy * SHARDS * sizeof(long long), st));
-            hipLaunchKernelGGL(k_set_hidx, dim3((s.nheavy + BLK - 1) / BLK), dim3(BLK), 0, st, s.nheavy,
-                               s.cls_list[NGC].p, s.hidx.p);
             KS_CHECK(hipStreamSynchronize(st));
         }
     }
@@ -1411,12 +1422,11 @@ int Engine::solve(ks_result& res, std::string& err) {
     // ------------------------------------------------------------ phases ---
     DG g = s.dg();
     const int fgrid = s.window_grid();
-    const int dgrid = fgrid;
-    const int ngrid = grid_for(n, 2048);
+    const int ngrid = grid_for(nn, 2048);
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
     gi = std::max(2, std::min(MAXB, gi)) & ~1;     // even: sweeps end on p0
-    const int pr_cap = 160;             // price-refinement rounds before giving up
+    const int pr_cap = 160;                        // price-refinement rounds before giving up
     const bool use_pr = s.opts.price_refine != 0;
     long long eps = std::max<long long>(1, (long long)s.maxc * mult);
     uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, cycles = 0;
@@ -1438,9 +1448,8 @@ int Engine::solve(ks_result& res, std::string& err) {
     auto bf_rounds = [&](bool pr, int k, bool first_dense) {
         for (int r = 0; r < k; ++r) {
             const int dense = (first_dense && r == 0) ? 1 : 0;
-            const int grid = dense ? dgrid : fgrid;
-            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
-            else hipLaunchKernelGGL(k_bf_round<false>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
+            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(fgrid), dim3(BLK), 0, st, g, bseq, dense);
+            else hipLaunchKernelGGL(k_bf_round<false>, dim3(fgrid), dim3(BLK), 0, st, g, bseq, dense);
             ++bseq;
             ++bf_launches;
         }
@@ -1475,7 +1484,7 @@ int Engine::solve(ks_result& res, std::string& err) {
         ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}, 0});
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(dgrid), dim3(BLK), 0, st, g);
+        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         bool gu_running = false;
         uint64_t phase_sweeps = 0;
@@ -1599,7 +1608,7 @@ int Engine::solve(ks_result& res, std::string& err) {
                 std::fprintf(f, "]}");
             }
             std::fprintf(f, "], ");
-            const char* names[4] = {"visits", "relabels", "medium", "heavy"};
+            const char* names[4] = {"visits", "relabels", "groups", "heavy"};
             for (int k = 0; k < 4; ++k) {
                 std::fprintf(f, "%s\"%s\": [", k ? "], " : "", names[k]);
                 for (uint64_t i = 0; i < nt; ++i) std::fprintf(f, "%s%u", i ? ", " : "", ht[4 * i + k]);
