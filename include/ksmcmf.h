@@ -76,11 +76,11 @@ extern "C" {
 typedef struct ks_ctx ks_ctx;
 
 typedef struct ks_opts {
-    int32_t  alpha;            /* cost-scaling factor per ε-phase (default 16)          */
+    int32_t  alpha;            /* cost-scaling factor per ε-phase (default 8)           */
     int32_t  verify;           /* run the on-device verifier after every solve (1)      */
     int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */
     int32_t  price_refine;     /* certify optimality early by price refinement (1)      */
-    int32_t  gu_interval;      /* sweeps between global price updates (default 8)       */
+    int32_t  gu_interval;      /* sweeps between global price updates (default 32)      */
     int32_t  reserved[11];
 } ks_opts;
 

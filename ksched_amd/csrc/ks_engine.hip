@@ -64,7 +64,7 @@ namespace {
 constexpr int BLK = 256;
 constexpr int WAVE = 64;
 constexpr int WPB = BLK / WAVE;
-constexpr int NGC = 5;             // group classes: 4, 8, 16, 32, 64 lanes per node
+constexpr int NGC = 6;             // group classes: 4, 8, 16, 32, 64 lanes; 64 lanes × several chunks
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
 constexpr int CHUNK = 256;         // heavy hubs: one residual arc per thread
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
@@ -97,10 +97,17 @@ struct HItem {
 
 __host__ __device__ constexpr int class_lanes(int c) { return c < 4 ? (4 << c) : 64; }
 __host__ __device__ inline int degree_class(int d) {
-    return d <= 4 ? 0 : d <= 8 ? 1 : d <= 16 ? 2 : d <= 32 ? 3 : d <= HEAVY_MIN ? 4 : NGC;
+    return d <= 4 ? 0 : d <= 8 ? 1 : d <= 16 ? 2 : d <= 32 ? 3 : d <= 64 ? 4 : d <= HEAVY_MIN ? 5 : NGC;
 }
+constexpr int CCLS = 5;            // chunked class: Bellman-Ford splits its nodes into 64-arc waves
+
+struct CItem {                     // one 64-arc chunk of a chunked-class node
+    int node, begin, end, lead;    // lead = 1 for the node's first chunk
+    int nch;                       // chunks of the node
+};
 // A wave owns one window: win_batches(c) batches of 64/G consecutive node ids.
 __host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
+static_assert(NGC == 6, "KS_BY_CLASS dispatches six classes");
 __host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
 
 // One frontier buffer: a flag byte per (non-hub) node, a flag per hub.
@@ -113,6 +120,7 @@ struct DG {
     int n;                 // internal node ids: [0, hub_base) grouped nodes, then hubs
     int m;
     int hub_base;
+    int expand;            // Bellman-Ford: relax low-degree targets two hops per round
     const int* first;
     const int* head;
     const int* rev;
@@ -130,6 +138,11 @@ struct DG {
     const HItem* hitems;
     int nhitems;
     int nheavy;
+    const CItem* citems;   // chunks of the chunked class
+    int ncitems;
+    long long* cmin;       // per chunked node: relabel minimum of this sweep
+    int* cunsat;           // per chunked node: some chunk left admissible capacity
+    int* carrive;          // per chunked node: chunks arrived this sweep
     const int* hnchunks;
     int* harrive;
     long long* hmin;
@@ -389,6 +402,7 @@ __device__ __forceinline__ long long block_excl_scan(long long x, long long* sh,
         else if (i_ < g.wbeg[3]) KS_WINDOW(2, ARGS, i_, CALLT(2))                    \
         else if (i_ < g.wbeg[4]) KS_WINDOW(3, ARGS, i_, CALLT(3))                    \
         else if (i_ < g.wbeg[5]) KS_WINDOW(4, ARGS, i_, CALLT(4))                    \
+        else if (i_ < g.wbeg[6]) KS_WINDOW(5, ARGS, i_, CALLT(5))                    \
     }
 struct Scan {
     unsigned char* flags;   // frontier flags to consume (sparse pass)
@@ -573,17 +587,17 @@ template <int G>
 __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v, const long long* __restrict__ P,
                                             long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
     const int lig = lane_id() & (G - 1);
-    long long e = 0;
-    if (v >= 0) e = g.excess[v];
-    const bool act = e > 0;
-    long long pv = 0;
+    long long e = 0, pv = 0;
     int b0 = 0, en = 0;
-    if (act) {
+    if (v >= 0) {
+        e = g.excess[v];
         pv = P[v];
         b0 = g.first[v];
         en = g.first[v + 1];
-        if (lig == 0) c.visit++;
     }
+    const bool act = e > 0;
+    if (!act) en = b0;
+    if (act && lig == 0) c.visit++;
     long long rem = e, minc = INF64;
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;   // G == 64: one node per wave
     for (int it = 0; it < iters; ++it) {
@@ -711,6 +725,74 @@ __device__ void heavy_chunk(const DG& g, const Front& nf, const HItem& it, const
     }
 }
 
+// Chunked-class discharge: one wave per 64-arc chunk of node x (flagged in F).
+// Chunks claim the node's excess with a CAS, push in parallel, report their
+// relabel minimum; the last-arriving chunk finalises the relabel and the flags.
+__device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, const CItem& ci,
+                                const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
+                                Pend& pd, int& out, Cnt& c) {
+    const int lane = lane_id();
+    const int x = ci.node;
+    const long long px = P[x];
+    const int a = ci.begin + lane;
+    long long r = 0, cr = 0;
+    int w = 0;
+    if (a < ci.end) {
+        r = g.rcap[a];
+        w = g.head[a];
+        cr = g.cost[a] + px - P[w];
+        c.scan++;
+    }
+    const long long adm = (a < ci.end && cr < 0 && r > 0) ? r : 0;
+    const long long incl = wave_incl_scan(adm, lane);
+    const long long Ac = __shfl(incl, WAVE - 1);
+    long long take = 0;
+    if (lane == 0) take = heavy_claim(&g.excess[x], Ac);
+    take = __shfl(take, 0);
+    long long d = take - (incl - adm);
+    d = d < 0 ? 0 : (d > adm ? adm : d);
+    if (d > 0) {
+        push_arc(g, &N, a, w, r, d, pd, out);
+        c.push++;
+    }
+    long long minc = INF64;
+    if (a < ci.end) {
+        if (cr < 0) {
+            if (r - d > 0) minc = cr;
+        } else if (r > 0 || cr <= eps) {
+            minc = cr;
+        }
+    }
+    flush_pending(g, &N, pd, out);
+    minc = wave_min(minc);
+    if (lane == 0) {
+        const int k = x - g.obeg[CCLS];
+        if (minc < INF64) atom_min(&g.cmin[k], minc);
+        if (take < Ac) atom_exch_i(&g.cunsat[k], 1);
+        drain_vm();
+        const int old = __hip_atomic_fetch_add(&g.carrive[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == ci.nch - 1) {
+            const long long mn = atom_exch(&g.cmin[k], INF64);
+            const int unsat = atom_exch_i(&g.cunsat[k], 0);
+            const long long ex = atom_load(&g.excess[x]);
+            long long np = px;
+            if (!unsat && ex > 0) {
+                if (mn >= INF64) g.ctl->infeasible = 1;
+                else np = px - (mn + eps);
+                c.relabel++;
+            }
+            c.visit++;
+            if (ex > 0) {
+                N.flag[x] = 1;
+                out = 1;
+            }
+            PN[x] = np;
+            F.flag[x] = 0;   // every chunk has read it
+            atom_exch_i(&g.carrive[k], 0);
+        }
+    }
+}
+
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx) {
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
@@ -727,10 +809,16 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
         const HItem it = g.hitems[blockIdx.x];
         if (F.hub[it.hid]) heavy_chunk(g, N, it, P, PN, eps, pd, out, c);
     } else {
-        const Scan sc{F.flag, 0};
+        const int w = wave_index_in_grid(g.nhitems);
+        if (w < g.wbeg[CCLS]) {
+            const Scan sc{F.flag, 0};
 #define KS_SWEEP_CALL(C) sweep_group<G_>(g, N, v, P, PN, eps, pd, out, c)
-        KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SWEEP_CALL)
+            KS_BY_CLASS(w, sc, KS_SWEEP_CALL)
 #undef KS_SWEEP_CALL
+        } else if (w - g.wbeg[CCLS] < g.ncitems) {
+            const CItem ci = g.citems[w - g.wbeg[CCLS]];
+            if (F.flag[ci.node]) chunk_discharge(g, F, N, ci, P, PN, eps, pd, out, c);
+        }
     }
     if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
     if (g.trace && tidx >= 0) {
@@ -755,17 +843,17 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
 // No returning atomics: a plain pre-check filters (a stale distance is only
 // larger), atomicMin commits, the flag store marks u for the next round.
 template <bool PR>
-__device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
-                                         long long eps, long long* hub_min, int& out) {
-    const long long rin = g.ucap[a] - g.rcap[a];
-    const int u = g.head[a];
-    const long long ca = g.cost[a];
-    if (rin <= 0) return;
-    const long long pu = g.p0[u];
-    const long long du = u < g.hub_base ? g.dist[u] : INF64;
+__device__ __forceinline__ long long arc_len(long long pu, long long ca, long long pv, long long eps) {
     long long len = floordiv(pu - ca - pv, eps) + 1;
     if (!PR) len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
-    const long long cand = dv + len;
+    return len;
+}
+
+// Offer distance cand to node u. Returns true when u is a grouped node whose
+// distance this call lowered (the caller then owns propagating it).
+template <bool PR>
+__device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long long cand, long long du,
+                                      long long* hub_min, int& out) {
     if (u >= g.hub_base) {
         const int h = u - g.hub_base;
         if (h < HUB_LDS) {
@@ -774,12 +862,53 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
             nf.hub[h] = 1;
             out = 1;
         }
-        return;
+        return false;
     }
-    if (cand >= du) return;
+    if (cand >= du) return false;
     atom_min(&g.dist[u], cand);
-    nf.flag[u] = 1;
-    out = 1;
+    return true;
+}
+
+// Relax the in-arcs of a low-degree node u (≤ 8 arcs: tasks, PUs) right after
+// its distance dropped to du: a second hop inside the same round.
+template <bool PR>
+__device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
+                                            long long eps, long long* hub_min, int& out) {
+    const int b0 = g.first[u], b1 = g.first[u + 1];
+    for (int b = b0; b < b1; ++b) {
+        const long long rin = g.ucap[b] - g.rcap[b];
+        const int u2 = g.head[b];
+        const long long cb = g.cost[b];
+        const long long pu2 = g.p0[u2];
+        const long long du2 = u2 < g.hub_base ? g.dist[u2] : INF64;
+        if (rin <= 0) continue;
+        const long long cand = du + arc_len<PR>(pu2, cb, pu, eps);
+        if (offer<PR>(g, nf, u2, cand, du2, hub_min, out)) {
+            nf.flag[u2] = 1;
+            out = 1;
+        }
+    }
+}
+
+// Relax in-arc (u→v) = reverse of CSR arc a = (v→u); residual ucap − rcap,
+// cost −cost(a). Loads are issued before the residual test (short chain).
+template <bool PR>
+__device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
+                                         long long eps, long long* hub_min, int& out) {
+    const long long rin = g.ucap[a] - g.rcap[a];
+    const int u = g.head[a];
+    const long long ca = g.cost[a];
+    const long long pu = g.p0[u];
+    const long long du = u < g.hub_base ? g.dist[u] : INF64;
+    if (rin <= 0) return;
+    const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
+    if (!offer<PR>(g, nf, u, cand, du, hub_min, out)) return;
+    if (g.expand && u < g.obeg[2]) {
+        expand_leaf<PR>(g, nf, u, cand, pu, eps, hub_min, out);   // tasks, PUs: two hops per round
+    } else {
+        nf.flag[u] = 1;
+        out = 1;
+    }
 }
 
 template <int G, bool PR>
@@ -838,10 +967,28 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
             }
         }
     } else {
-        const Scan sc{F.flag, dense};
+        const int w = wave_index_in_grid(g.nhitems);
+        if (w < g.wbeg[CCLS]) {
+            const Scan sc{F.flag, dense};
 #define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, hub_min, out, scans)
-        KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_BF_CALL)
+            KS_BY_CLASS(w, sc, KS_BF_CALL)
 #undef KS_BF_CALL
+        } else if (w - g.wbeg[CCLS] < g.ncitems) {
+            // chunked class: one 64-arc chunk per wave; the flag is read by every
+            // chunk of the node, and cleared by its lead chunk two rounds later
+            const CItem ci = g.citems[w - g.wbeg[CCLS]];
+            if (ci.lead && lane_id() == 0) g.bf[(seq + 2) % 3].flag[ci.node] = 0;
+            if (dense || F.flag[ci.node]) {
+                const long long dv = g.dist[ci.node];
+                if (PR || dv < INF64) {
+                    const int a = ci.begin + lane_id();
+                    if (a < ci.end) {
+                        relax_in<PR>(g, N, a, dv, g.p0[ci.node], eps, hub_min, out);
+                        scans++;
+                    }
+                }
+            }
+        }
     }
     __syncthreads();
     if (threadIdx.x < HUB_LDS && (int)threadIdx.x < g.nheavy) {
@@ -1074,6 +1221,9 @@ struct EngineImpl {
     DBuf<int> cls_list[NGC + 1];   // original ids of each degree class; [NGC] = heavy hubs
     DBuf<unsigned char> sel_tmp;
     DBuf<HItem> hitems;
+    DBuf<CItem> citems;
+    DBuf<long long> cmin;
+    DBuf<int> cunsat, carrive;
     DBuf<int> hnchunks, harrive, hunsat;
     DBuf<long long> hmin, inbox, part, flows;
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
@@ -1084,7 +1234,7 @@ struct EngineImpl {
     Ctl* h_ctl = nullptr;       // pinned host mirror
     long long* h_scr = nullptr; // pinned scratch: [0] eps
     int ncls[NGC + 1] = {0};
-    int nheavy = 0, nhitems = 0;
+    int nheavy = 0, nhitems = 0, ncitems = 0;
     int hub_base = 0, nn = 0;   // grouped node ids [0, hub_base), hubs after: nn ids
     int obeg[NGC + 1] = {0}, oend[NGC] = {0}, wbeg[NGC + 1] = {0};
     bool solved = false;
@@ -1100,7 +1250,7 @@ struct EngineImpl {
         rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release();
         dist.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
-        sel_tmp.release(); hitems.release(); hnchunks.release(); harrive.release(); hunsat.release();
+        sel_tmp.release(); hitems.release(); citems.release(); cmin.release(); cunsat.release(); carrive.release(); hnchunks.release(); harrive.release(); hunsat.release();
         hmin.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
         ctr.release(); trace.release(); ctl.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
@@ -1133,6 +1283,11 @@ struct EngineImpl {
         for (int c = 0; c < NGC; ++c) g.oend[c] = oend[c];
         g.hitems = hitems.p;
         g.nhitems = nhitems;
+        g.citems = citems.p;
+        g.ncitems = ncitems;
+        g.cmin = cmin.p;
+        g.cunsat = cunsat.p;
+        g.carrive = carrive.p;
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
         g.harrive = harrive.p;
@@ -1151,6 +1306,7 @@ struct EngineImpl {
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
+    int bf_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
 };
 
 #define KS_CHECK(expr)                                                   \
@@ -1417,11 +1573,45 @@ int Engine::solve(ks_result& res, std::string& err) {
             KS_CHECK(hipStreamSynchronize(st));
         }
     }
+    {
+        // chunked class: 64-arc chunk table (built on host from the class's CSR ranges)
+        const int c0 = s.obeg[CCLS], cn = s.ncls[CCLS];
+        std::vector<int> cf(cn + 1);
+        if (cn) {
+            KS_CHECK(hipMemcpyAsync(cf.data(), s.first.p + c0, (cn + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+            KS_CHECK(hipStreamSynchronize(st));
+        }
+        std::vector<CItem> ci;
+        for (int k = 0; k < cn; ++k) {
+            const int nch = (cf[k + 1] - cf[k] + 63) / 64;
+            for (int b = cf[k]; b < cf[k + 1]; b += 64)
+                ci.push_back(CItem{c0 + k, b, std::min(b + 64, cf[k + 1]), b == cf[k] ? 1 : 0, nch});
+        }
+        s.ncitems = (int)ci.size();
+        KS_CHECK(s.citems.ensure(std::max<size_t>(1, ci.size())));
+        KS_CHECK(s.cmin.ensure(std::max(1, cn)));
+        KS_CHECK(s.cunsat.ensure(std::max(1, cn)));
+        KS_CHECK(s.carrive.ensure(std::max(1, cn)));
+        if (!ci.empty())
+            KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
+        if (cn) {
+            std::vector<long long> cm(cn, INF64);
+            KS_CHECK(hipMemcpyAsync(s.cmin.p, cm.data(), cn * sizeof(long long), hipMemcpyHostToDevice, st));
+            KS_CHECK(hipMemsetAsync(s.cunsat.p, 0, cn * sizeof(int), st));
+            KS_CHECK(hipMemsetAsync(s.carrive.p, 0, cn * sizeof(int), st));
+            KS_CHECK(hipStreamSynchronize(st));
+        }
+    }
     KS_CHECK(hipEventRecord(s.ev[1], st));
 
     // ------------------------------------------------------------ phases ---
     DG g = s.dg();
+    {
+        const char* ex = std::getenv("KS_EXPAND");
+        g.expand = ex ? std::atoi(ex) : 0;
+    }
     const int fgrid = s.window_grid();
+    const int bgrid = s.bf_grid();
     const int ngrid = grid_for(nn, 2048);
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
@@ -1448,8 +1638,8 @@ int Engine::solve(ks_result& res, std::string& err) {
     auto bf_rounds = [&](bool pr, int k, bool first_dense) {
         for (int r = 0; r < k; ++r) {
             const int dense = (first_dense && r == 0) ? 1 : 0;
-            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(fgrid), dim3(BLK), 0, st, g, bseq, dense);
-            else hipLaunchKernelGGL(k_bf_round<false>, dim3(fgrid), dim3(BLK), 0, st, g, bseq, dense);
+            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(bgrid), dim3(BLK), 0, st, g, bseq, dense);
+            else hipLaunchKernelGGL(k_bf_round<false>, dim3(bgrid), dim3(BLK), 0, st, g, bseq, dense);
             ++bseq;
             ++bf_launches;
         }
@@ -1502,7 +1692,7 @@ int Engine::solve(ks_result& res, std::string& err) {
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             for (int k = 0; k < gi; ++k) {
                 const long long ti = (long long)sweep_launches + k;
-                hipLaunchKernelGGL(k_sweep, dim3(fgrid), dim3(BLK), 0, st, g, k, sseq + k,
+                hipLaunchKernelGGL(k_sweep, dim3(bgrid), dim3(BLK), 0, st, g, k, sseq + k,
                                    (g.trace && ti < kTraceMax) ? (int)ti : -1);
             }
             KS_CHECK(read_ctl());

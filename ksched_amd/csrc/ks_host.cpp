@@ -251,11 +251,11 @@ int ks_abi_version(void) { return KSMCMF_ABI_VERSION; }
 void ks_default_opts(ks_opts* o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
-    o->alpha = 16;
+    o->alpha = 8;
     o->verify = 1;
     o->auto_sink = 1;
     o->price_refine = 1;
-    o->gu_interval = 8;
+    o->gu_interval = 32;
 }
 
 ks_ctx* ks_create(int device, const ks_opts* opts) {

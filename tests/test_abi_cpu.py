@@ -34,7 +34,7 @@ def test_abi_version_and_default_opts():
     lib = native.load()
     assert lib.ks_abi_version() == 1
     o = native.default_opts()
-    assert (o.alpha, o.verify, o.auto_sink) == (16, 1, 1)
+    assert (o.alpha, o.verify, o.auto_sink) == (8, 1, 1)
     assert o.price_refine == 1 and o.gu_interval > 0
 
 

@@ -25,10 +25,10 @@ struct G {
 static i64 floordiv(i64 a, i64 b) { i64 q = a / b; if ((a % b) && (a < 0)) --q; return q; }
 
 struct Opt {
-    int alpha = 16, gi = 48, precise = 0, early_gu = 0, verbose = 1, sat_eps = 0, pref = 0, bfk = 0;
+    int alpha = 16, gi = 48, precise = 0, early_gu = 0, verbose = 1, sat_eps = 0, pref = 0, bfk = 0, tailT = 0;
 };
 
-struct Stats { i64 sweeps = 0, gus = 0, bf_rounds = 0, visits = 0, relabels = 0, gu_scans = 0, gu_settled = 0; };
+struct Stats { i64 tail_sweeps = 0, sweeps = 0, gus = 0, bf_rounds = 0, visits = 0, relabels = 0, gu_scans = 0, gu_settled = 0; };
 
 // global update: Dijkstra from deficits, length floor(rc/eps)+1; returns max hops
 static int gu(G& g, i64 eps, bool early, Stats& st) {
@@ -159,6 +159,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "-s")) o.sat_eps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-r")) o.pref = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-k")) o.bfk = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-t")) o.tailT = atoi(argv[++i]);
     }
     int64_t n, m;
     ko_quincy_sizes(T, M, R, J, &n, &m);
@@ -212,6 +213,8 @@ int main(int argc, char** argv) {
             for (int v = 0; v < n; ++v) { esnap[v] = g.excess[v]; act[v] = esnap[v] > 0; nact += act[v]; }
             if (!nact) break;
             ph.sweeps++;
+            const bool tail = o.tailT && nact <= o.tailT;
+            if (tail) ph.tail_sweeps++;
             if (getenv("SIM_DUMP") && eps == atoll(getenv("SIM_DUMP")) && ph.sweeps >= 300 && ph.sweeps < 306) {
                 int cnt[6] = {0};
                 i64 ex[6] = {0};
@@ -248,13 +251,14 @@ int main(int argc, char** argv) {
                 }
             }
             for (int v = 0; v < n; ++v) g.P[v] = g.PN[v];
+            if (tail) since = 0;
             if (++since >= o.gi) { if (o.bfk) gu_bf(g, eps, o.bfk, ph); else gu(g, eps, o.early_gu, ph); since = 0; }
             if (ph.sweeps > 2000000) { fprintf(stderr, "no convergence\n"); return 1; }
         }
         if (o.verbose)
-            printf("eps=%lld sweeps=%lld gus=%lld bf_rounds=%lld visits=%lld relabels=%lld gu_settled/gu=%lld gu_scans/gu=%lld\n", eps, ph.sweeps, ph.gus,
+            printf("eps=%lld tail=%lld sweeps=%lld gus=%lld bf_rounds=%lld visits=%lld relabels=%lld gu_settled/gu=%lld gu_scans/gu=%lld\n", eps, ph.tail_sweeps, ph.sweeps, ph.gus,
                    ph.bf_rounds, ph.visits, ph.relabels, ph.gu_settled / std::max<i64>(1, ph.gus), ph.gu_scans / std::max<i64>(1, ph.gus));
-        tot.sweeps += ph.sweeps; tot.gus += ph.gus; tot.bf_rounds += ph.bf_rounds; tot.visits += ph.visits;
+        tot.sweeps += ph.sweeps; tot.tail_sweeps += ph.tail_sweeps; tot.gus += ph.gus; tot.bf_rounds += ph.bf_rounds; tot.visits += ph.visits;
         tot.relabels += ph.relabels;
     } while (eps > 1);
     i64 c = 0;
@@ -265,6 +269,6 @@ int main(int argc, char** argv) {
         for (i64 i = 0; i < m; ++i) { int s = src[i] - 1, d = dst[i] - 1; isf[p2[s]++] = 1; p2[d]++; }
     }
     for (i64 a = 0; a < 2 * m; ++a) if (isf[a]) c += g.rcap[g.rev[a]] * (g.cost[a] / mult);
-    printf("TOTAL sat_eps=%d alpha=%d gi=%d precise=%d early=%d: cost=%lld sweeps=%lld gus=%lld bf_rounds=%lld visits=%lld relabels=%lld\n",
-           o.sat_eps, o.alpha, o.gi, o.precise, o.early_gu, c, tot.sweeps, tot.gus, tot.bf_rounds, tot.visits, tot.relabels);
+    printf("TOTAL tail=%lld sat_eps=%d alpha=%d gi=%d precise=%d early=%d: cost=%lld sweeps=%lld gus=%lld bf_rounds=%lld visits=%lld relabels=%lld\n",
+           tot.tail_sweeps, o.sat_eps, o.alpha, o.gi, o.precise, o.early_gu, c, tot.sweeps, tot.gus, tot.bf_rounds, tot.visits, tot.relabels);
 }
