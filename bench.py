@@ -69,7 +69,11 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     t0 = time.perf_counter()
-    results = [ctx.solve() for _ in range(args.steps)]
+    results, step_ms = [], []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        results.append(ctx.solve())
+        step_ms.append(1e3 * (time.perf_counter() - ts))
     if dist:
         torch.cuda.synchronize()
         dist.barrier()
@@ -131,6 +135,7 @@ def main():
                                    f"(n={g.n}, m={g.m}), full device re-solve per step, one graph per GPU",
                        "tasks": T, "machines": M, "racks": R, "jobs": J, "seed": seed, "n": g.n, "m": g.m,
                        "parallelism": f"independent graphs x{world}"},
+            "step_ms": [round(x, 2) for x in step_ms],
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "gather": gather,
             "solve": {k: v for k, v in last.items()}}
     if rank == 0:

@@ -66,7 +66,9 @@ constexpr int WAVE = 64;
 constexpr int WPB = BLK / WAVE;
 constexpr int NGC = 6;             // group classes: 4, 8, 16, 32, 64 lanes; 64 lanes × several chunks
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
-constexpr int CHUNK = 256;         // heavy hubs: one residual arc per thread
+constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
+constexpr int PER_T = CHUNK / 256; // arcs per thread in a hub chunk
+constexpr int WPW = 4;             // windows per wave in sparse (grid-stride) passes
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -140,18 +142,19 @@ struct DG {
     int nheavy;
     const CItem* citems;   // chunks of the chunked class
     int ncitems;
-    long long* cmin;       // per chunked node: relabel minimum of this sweep
-    int* cunsat;           // per chunked node: some chunk left admissible capacity
-    int* carrive;          // per chunked node: chunks arrived this sweep
     const int* hnchunks;
-    int* harrive;
-    long long* hmin;
-    int* hunsat;
+    long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
+    long long* q_taken;
+    long long* q_min;
+    int* q_unsat;
+    int* q_arrive;
     Front sf[3];   // sweep frontiers
     Front bf[3];   // Bellman-Ford frontiers
     Ctl* ctl;
     unsigned long long* ctr;
     unsigned* trace;   // optional per-sweep [visits, relabels, groups, heavy] (KS_TRACE)
+    unsigned long long* stamps;   // optional per-block [t0, t1, kind|active] of one sweep (KS_STAMP)
+    int stamp_sweep;
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -554,15 +557,18 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
         const HItem it = g.hitems[blockIdx.x];
         const long long px = P[it.node];
         long long tot = 0;
-        const int a = it.begin + threadIdx.x;
-        if (a < it.end) {
-            const long long r = g.rcap[a];
-            if (r > 0) {
-                const int w = g.head[a];
-                if (g.cost[a] + px - P[w] < 0) {
-                    push_arc(g, nullptr, a, w, r, r, pd, out);
-                    tot += r;
-                    c.push++;
+#pragma unroll
+        for (int k = 0; k < PER_T; ++k) {
+            const int a = it.begin + threadIdx.x * PER_T + k;
+            if (a < it.end) {
+                const long long r = g.rcap[a];
+                if (r > 0) {
+                    const int w = g.head[a];
+                    if (g.cost[a] + px - P[w] < 0) {
+                        push_arc(g, nullptr, a, w, r, r, pd, out);
+                        tot += r;
+                        c.push++;
+                    }
                 }
             }
         }
@@ -584,17 +590,11 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
 // One node per G-lane group, one residual arc per lane; admissible capacity is
 // distributed by an in-group prefix sum, the relabel minimum by a group min.
 template <int G>
-__device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v, const long long* __restrict__ P,
-                                            long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
+__device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v, long long e, long long pv, int b0,
+                                            int en, long long* __restrict__ PN, const long long* __restrict__ P,
+                                            long long eps, Pend& pd, int& out, Cnt& c) {
     const int lig = lane_id() & (G - 1);
-    long long e = 0, pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        e = g.excess[v];
-        pv = P[v];
-        b0 = g.first[v];
-        en = g.first[v + 1];
-    }
+    if (v < 0) e = 0;
     const bool act = e > 0;
     if (!act) en = b0;
     if (act && lig == 0) c.visit++;
@@ -647,93 +647,124 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
     }
 }
 
-__device__ long long heavy_claim(long long* ex, long long want) {
-    if (want <= 0) return 0;
-    long long old = atom_add_ret(ex, 0);
-    for (;;) {
-        if (old <= 0) return 0;
-        const long long take = old < want ? old : want;
-        if (__hip_atomic_compare_exchange_strong(ex, &old, old - take, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return take;
-    }
+// -------------------------------------------------- chunked claim protocol ---
+// Hubs (one workgroup per 1024-arc chunk) and chunked-class nodes (one wave per
+// 64-arc chunk) discharge cooperatively. Every chunk reads the node's excess E
+// once, requests its admissible capacity Ac with ONE returning atomicAdd on the
+// node's request counter (no CAS loop), takes clamp(E − start, 0, Ac), pushes,
+// and reports (taken, relabel minimum, unsaturated). The last-arriving chunk
+// settles the node: subtracts what was taken, drains the hub inbox, relabels if
+// every admissible arc was saturated and excess is left, and marks it active.
+// Concurrent inflows only ever add excess, so Σ taken ≤ the excess present.
+__device__ __forceinline__ long long claim(const DG& g, int slot, long long E, long long Ac) {
+    if (Ac <= 0) return 0;
+    const long long start = __hip_atomic_fetch_add(&g.q_req[slot], Ac, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long take = E - start;
+    return take < 0 ? 0 : (take > Ac ? Ac : take);
 }
 
-__device__ void heavy_chunk(const DG& g, const Front& nf, const HItem& it, const long long* __restrict__ P,
-                            long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
+// One lane per chunk. Returns nothing; settles the node when it arrives last.
+__device__ __forceinline__ void settle(const DG& g, const Front& F, const Front& N, int slot, int x, int nch,
+                                       bool hub, long long take, long long Ac, long long minc, long long px,
+                                       long long* __restrict__ PN, long long eps, int& out, Cnt& c) {
+    if (minc < INF64) atom_min(&g.q_min[slot], minc);
+    if (take < Ac) atom_exch_i(&g.q_unsat[slot], 1);
+    if (take) atom_add(&g.q_taken[slot], take);
+    drain_vm();
+    const int old = __hip_atomic_fetch_add(&g.q_arrive[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != nch - 1) return;
+    const long long mn = atom_exch(&g.q_min[slot], INF64);
+    const int unsat = atom_exch_i(&g.q_unsat[slot], 0);
+    const long long taken = atom_exch(&g.q_taken[slot], 0);
+    atom_exch(&g.q_req[slot], 0LL);
+    if (taken) atom_add(&g.excess[x], -taken);
+    if (hub) drain_inbox(g, x - g.hub_base);
+    const long long now = atom_load(&g.excess[x]);
+    long long np = px;
+    if (!unsat && now > 0) {
+        if (mn >= INF64) g.ctl->infeasible = 1;
+        else np = px - (mn + eps);
+        c.relabel++;
+    }
+    c.visit++;
+    PN[x] = np;
+    if (now > 0) mark(g, N, x, out);
+    if (!hub) F.flag[x] = 0;   // every chunk has read it
+    atom_exch_i(&g.q_arrive[slot], 0);
+}
+
+// Hub chunk: one workgroup, 1024 arcs (four per thread, loads issued together).
+__device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HItem& it,
+                          const long long* __restrict__ P, long long* __restrict__ PN, long long eps, Pend& pd,
+                          int& out, Cnt& c) {
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
-    const int x = it.node, h = it.hid;
-    const bool chunk0 = it.begin == g.first[x];
-    if (chunk0 && threadIdx.x == 0) drain_inbox(g, h);
+    const int x = it.node;
     const long long px = P[x];
-    const int a = it.begin + threadIdx.x;
-    long long r = 0, cr = 0;
-    int w = 0;
-    if (a < it.end) {
-        r = g.rcap[a];
-        w = g.head[a];
-        cr = g.cost[a] + px - P[w];
-        c.scan++;
+    const long long E = g.excess[x];
+    long long r[PER_T], cr[PER_T], adm[PER_T];
+    int w[PER_T];
+    long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        r[k] = 0;
+        w[k] = 0;
+        if (a < it.end) {
+            r[k] = g.rcap[a];
+            w[k] = g.head[a];
+        }
     }
-    const long long adm = (a < it.end && cr < 0 && r > 0) ? r : 0;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        cr[k] = 0;
+        if (a < it.end) {
+            cr[k] = g.cost[a] + px - P[w[k]];
+            c.scan++;
+        }
+        adm[k] = (a < it.end && cr[k] < 0 && r[k] > 0) ? r[k] : 0;
+        mine += adm[k];
+    }
     long long Ac = 0;
-    const long long excl = block_excl_scan(adm, sh, &Ac);
-    if (threadIdx.x == 0) s_take = heavy_claim(&g.excess[x], Ac);
+    const long long excl = block_excl_scan(mine, sh, &Ac);
+    if (threadIdx.x == 0) s_take = claim(g, it.hid, E, Ac);
     __syncthreads();
     const long long take = s_take;
-    long long d = take - excl;
-    d = d < 0 ? 0 : (d > adm ? adm : d);
-    if (d > 0) {
-        push_arc(g, &nf, a, w, r, d, pd, out);
-        c.push++;
-    }
+    long long rt = take - excl;
+    rt = rt < 0 ? 0 : (rt > mine ? mine : rt);
     long long minc = INF64;
-    if (a < it.end) {
-        if (cr < 0) {
-            if (r - d > 0) minc = cr;
-        } else if (r > 0 || cr <= eps) {
-            minc = cr;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        const long long d = adm[k] < rt ? adm[k] : rt;
+        rt -= d;
+        if (d > 0) {
+            push_arc(g, &N, a, w[k], r[k], d, pd, out);
+            c.push++;
+        }
+        if (a < it.end) {
+            if (cr[k] < 0) {
+                if (r[k] - d > 0) minc = min(minc, cr[k]);
+            } else if (r[k] > 0 || cr[k] <= eps) {
+                minc = min(minc, cr[k]);
+            }
         }
     }
-    flush_pending(g, &nf, pd, out);
+    flush_pending(g, &N, pd, out);
     minc = block_min(minc, sh);
-    if (threadIdx.x == 0) {
-        if (minc < INF64) atom_min_ret(&g.hmin[h], minc);
-        if (take < Ac) atom_exch_i(&g.hunsat[h], 1);
-        drain_vm();
-        const int old = __hip_atomic_fetch_add(&g.harrive[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == g.hnchunks[h] - 1) {
-            // last chunk of hub x in this sweep: finalise
-            const long long mn = atom_exch(&g.hmin[h], INF64);
-            const int unsat = atom_exch_i(&g.hunsat[h], 0);
-            const long long ex = atom_add_ret(&g.excess[x], 0);
-            long long np = px;
-            if (!unsat && ex > 0) {
-                if (mn >= INF64) g.ctl->infeasible = 1;
-                else np = px - (mn + eps);
-                c.relabel++;
-            }
-            if (ex > 0) {
-                nf.hub[h] = 1;
-                out = 1;
-                c.visit++;
-            }
-            PN[x] = np;
-            atom_exch_i(&g.harrive[h], 0);
-        }
-    }
+    if (threadIdx.x == 0)
+        settle(g, F, N, it.hid, x, g.hnchunks[it.hid], true, take, Ac, minc, px, PN, eps, out, c);
 }
 
 // Chunked-class discharge: one wave per 64-arc chunk of node x (flagged in F).
-// Chunks claim the node's excess with a CAS, push in parallel, report their
-// relabel minimum; the last-arriving chunk finalises the relabel and the flags.
 __device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, const CItem& ci,
                                 const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
                                 Pend& pd, int& out, Cnt& c) {
     const int lane = lane_id();
     const int x = ci.node;
     const long long px = P[x];
+    const long long E = g.excess[x];
     const int a = ci.begin + lane;
     long long r = 0, cr = 0;
     int w = 0;
@@ -746,8 +777,9 @@ __device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, con
     const long long adm = (a < ci.end && cr < 0 && r > 0) ? r : 0;
     const long long incl = wave_incl_scan(adm, lane);
     const long long Ac = __shfl(incl, WAVE - 1);
+    const int slot = g.nheavy + (x - g.obeg[CCLS]);
     long long take = 0;
-    if (lane == 0) take = heavy_claim(&g.excess[x], Ac);
+    if (lane == 0) take = claim(g, slot, E, Ac);
     take = __shfl(take, 0);
     long long d = take - (incl - adm);
     d = d < 0 ? 0 : (d > adm ? adm : d);
@@ -765,31 +797,62 @@ __device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, con
     }
     flush_pending(g, &N, pd, out);
     minc = wave_min(minc);
-    if (lane == 0) {
-        const int k = x - g.obeg[CCLS];
-        if (minc < INF64) atom_min(&g.cmin[k], minc);
-        if (take < Ac) atom_exch_i(&g.cunsat[k], 1);
-        drain_vm();
-        const int old = __hip_atomic_fetch_add(&g.carrive[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == ci.nch - 1) {
-            const long long mn = atom_exch(&g.cmin[k], INF64);
-            const int unsat = atom_exch_i(&g.cunsat[k], 0);
-            const long long ex = atom_load(&g.excess[x]);
-            long long np = px;
-            if (!unsat && ex > 0) {
-                if (mn >= INF64) g.ctl->infeasible = 1;
-                else np = px - (mn + eps);
-                c.relabel++;
-            }
-            c.visit++;
-            if (ex > 0) {
-                N.flag[x] = 1;
-                out = 1;
-            }
-            PN[x] = np;
-            F.flag[x] = 0;   // every chunk has read it
-            atom_exch_i(&g.carrive[k], 0);
+    if (lane == 0) settle(g, F, N, slot, x, ci.nch, false, take, Ac, minc, px, PN, eps, out, c);
+}
+
+// ------------------------------------------------------ grid-stride windows ---
+// Sparse passes use a one-generation grid: each wave owns WPW windows (class
+// windows, then chunk items) strided across the grid, ballots all their flags
+// first (independent loads), then processes only the active ones.
+__device__ __forceinline__ int class_of_window(const DG& g, int w) {
+    int c = 0;
+#pragma unroll
+    for (int k = 1; k < CCLS; ++k) c += (w >= g.wbeg[k]) ? 1 : 0;
+    return c;
+}
+
+// Ballot of window w's flags. Class windows clear what they read (if clear);
+// chunk items only read (their node's flag is cleared by the node's owner).
+__device__ __forceinline__ unsigned long long window_mask(const DG& g, unsigned char* flags, int w, bool clear) {
+    bool on = false;
+    const int ln = lane_id();
+    if (w < g.wbeg[CCLS]) {
+        const int c = class_of_window(g, w);
+        const int ws = c < 4 ? (32 >> c) : 1;
+        const int slot = g.obeg[c] + (w - g.wbeg[c]) * ws + ln;
+        if (ln < ws) {
+            on = flags[slot] != 0;
+            if (on && clear) flags[slot] = 0;
         }
+    } else if (w < g.wbeg[CCLS] + g.ncitems) {
+        if (ln == 0) on = flags[g.citems[w - g.wbeg[CCLS]].node] != 0;
+    }
+    return __ballot(on);
+}
+
+template <int C>
+__device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, unsigned long long mask,
+                                          const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
+                                          Pend& pd, int& out, Cnt& c) {
+    constexpr int G = class_lanes(C);
+    constexpr int PER = 64 / G;
+    constexpr int WS = win_slots(C);
+    const int base = g.obeg[C] + (w - g.wbeg[C]) * WS;
+    const int k = lane_id() / G;
+    while (mask) {
+        unsigned long long mm = mask;
+        for (int j = 0; j < k; ++j) mm &= mm - 1;
+        const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
+        long long e = 0, pv = 0;
+        int b0 = 0, en = 0;
+        if (v >= 0) {
+            e = g.excess[v];
+            pv = P[v];
+            b0 = g.first[v];
+            en = g.first[v + 1];
+        }
+        sweep_group<G>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
+        for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
 }
 
@@ -802,25 +865,50 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
     const long long eps = g.ctl->eps;
     const long long* P = (pos & 1) ? g.p1 : g.p0;
     long long* PN = (pos & 1) ? g.p0 : g.p1;
+    const bool stamp = g.stamps && tidx == g.stamp_sweep;
+    const unsigned long long ts0 = stamp ? __builtin_amdgcn_s_memrealtime() : 0;
     Pend pd{-1, 0};
     Cnt c;
     int out = 0;
     if ((int)blockIdx.x < g.nhitems) {
         const HItem it = g.hitems[blockIdx.x];
-        if (F.hub[it.hid]) heavy_chunk(g, N, it, P, PN, eps, pd, out, c);
+        if (F.hub[it.hid]) hub_chunk(g, F, N, it, P, PN, eps, pd, out, c);
     } else {
-        const int w = wave_index_in_grid(g.nhitems);
-        if (w < g.wbeg[CCLS]) {
-            const Scan sc{F.flag, 0};
-#define KS_SWEEP_CALL(C) sweep_group<G_>(g, N, v, P, PN, eps, pd, out, c)
-            KS_BY_CLASS(w, sc, KS_SWEEP_CALL)
-#undef KS_SWEEP_CALL
-        } else if (w - g.wbeg[CCLS] < g.ncitems) {
-            const CItem ci = g.citems[w - g.wbeg[CCLS]];
-            if (F.flag[ci.node]) chunk_discharge(g, F, N, ci, P, PN, eps, pd, out, c);
+        const int tw = ((int)gridDim.x - g.nhitems) * WPB;
+        const int w0 = wave_index_in_grid(g.nhitems);
+        unsigned long long mk[WPW];
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) mk[j] = window_mask(g, F.flag, w0 + j * tw, true);
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            if (!mk[j]) continue;
+            const int w = w0 + j * tw;
+            if (w >= g.wbeg[CCLS]) {
+                chunk_discharge(g, F, N, g.citems[w - g.wbeg[CCLS]], P, PN, eps, pd, out, c);
+                continue;
+            }
+            switch (class_of_window(g, w)) {
+                case 0: sweep_win<0>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+                case 1: sweep_win<1>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+                case 2: sweep_win<2>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+                case 3: sweep_win<3>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+                default: sweep_win<4>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+            }
         }
     }
     if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
+    if (stamp) {
+        const int busy = __syncthreads_or(c.visit > 0 || c.scan > 0);
+        if (threadIdx.x == 0) {
+            const int w0 = wave_index_in_grid(g.nhitems);
+            int kind = (int)blockIdx.x < g.nhitems ? 7 : (w0 >= g.wbeg[CCLS] ? 6 : 0);
+            for (int k = 1; k <= CCLS && kind == 0; ++k)
+                if (w0 < g.wbeg[k]) kind = k;   // window class + 1
+            g.stamps[3 * blockIdx.x] = ts0;
+            g.stamps[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+            g.stamps[3 * blockIdx.x + 2] = (unsigned long long)kind | ((unsigned long long)busy << 8);
+        }
+    }
     if (g.trace && tidx >= 0) {
         const long long v = wave_sum(c.visit), r = wave_sum(c.relabel);
         if (lane_id() == 0 && (v | r)) {
@@ -912,6 +1000,61 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
 }
 
 template <int G, bool PR>
+__device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v, long long dv, long long pv, int b0,
+                                             int en, long long eps, long long* hub_min, int& out, long long& scans) {
+    const int lig = lane_id() & (G - 1);
+    const bool act = v >= 0 && (PR || dv < INF64);
+    if (!act) en = b0;
+    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
+    for (int it = 0; it < iters; ++it) {
+        const int a = b0 + it * G + lig;
+        if (a < en) {
+            relax_in<PR>(g, nf, a, dv, pv, eps, hub_min, out);
+            scans++;
+        }
+    }
+}
+
+// Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
+template <int C, bool PR>
+__device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, long long eps,
+                                       long long* hub_min, int& out, long long& scans) {
+    constexpr int G = class_lanes(C);
+    constexpr int PER = 64 / G;
+    constexpr int WS = win_slots(C);
+    const int base = g.obeg[C] + (w - g.wbeg[C]) * WS;
+    const int k = lane_id() / G;
+    while (mask) {
+        unsigned long long mm = mask;
+        for (int j = 0; j < k; ++j) mm &= mm - 1;
+        const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
+        long long d = INF64, pv = 0;
+        int b0 = 0, en = 0;
+        if (v >= 0) {
+            d = g.dist[v];
+            pv = g.p0[v];
+            b0 = g.first[v];
+            en = g.first[v + 1];
+        }
+        bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, hub_min, out, scans);
+        for (int j = 0; j < PER; ++j) mask &= mask - 1;
+    }
+}
+
+// One 64-arc chunk of a chunked-class node (its flag already tested).
+template <bool PR>
+__device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
+                                         long long* hub_min, int& out, long long& scans) {
+    const long long dv = g.dist[ci.node];
+    if (!PR && dv >= INF64) return;
+    const int a = ci.begin + lane_id();
+    if (a < ci.end) {
+        relax_in<PR>(g, N, a, dv, g.p0[ci.node], eps, hub_min, out);
+        scans++;
+    }
+}
+
+template <int G, bool PR>
 __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long* hub_min,
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
@@ -959,34 +1102,56 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
         if (dense || F.hub[it.hid]) {
             const long long dv = atom_load(&g.dist[it.node]);
             if (PR || dv < INF64) {
-                const int a = it.begin + threadIdx.x;
-                if (a < it.end) {
-                    relax_in<PR>(g, N, a, dv, g.p0[it.node], eps, hub_min, out);
-                    scans++;
+                const long long pv = g.p0[it.node];
+#pragma unroll
+                for (int k = 0; k < PER_T; ++k) {
+                    const int a = it.begin + threadIdx.x * PER_T + k;
+                    if (a < it.end) {
+                        relax_in<PR>(g, N, a, dv, pv, eps, hub_min, out);
+                        scans++;
+                    }
                 }
             }
         }
-    } else {
+    } else if (dense) {
         const int w = wave_index_in_grid(g.nhitems);
         if (w < g.wbeg[CCLS]) {
-            const Scan sc{F.flag, dense};
+            const Scan sc{F.flag, 1};
 #define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, hub_min, out, scans)
             KS_BY_CLASS(w, sc, KS_BF_CALL)
 #undef KS_BF_CALL
         } else if (w - g.wbeg[CCLS] < g.ncitems) {
-            // chunked class: one 64-arc chunk per wave; the flag is read by every
-            // chunk of the node, and cleared by its lead chunk two rounds later
-            const CItem ci = g.citems[w - g.wbeg[CCLS]];
-            if (ci.lead && lane_id() == 0) g.bf[(seq + 2) % 3].flag[ci.node] = 0;
-            if (dense || F.flag[ci.node]) {
-                const long long dv = g.dist[ci.node];
-                if (PR || dv < INF64) {
-                    const int a = ci.begin + lane_id();
-                    if (a < ci.end) {
-                        relax_in<PR>(g, N, a, dv, g.p0[ci.node], eps, hub_min, out);
-                        scans++;
-                    }
-                }
+            bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
+        }
+    } else {
+        const int tw = ((int)gridDim.x - g.nhitems) * WPB;
+        const int w0 = wave_index_in_grid(g.nhitems);
+        unsigned long long mk[WPW];
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            const int w = w0 + j * tw;
+            mk[j] = window_mask(g, F.flag, w, true);
+            // chunk items: a node's flag is read by all its chunks; the lead chunk
+            // clears it two rounds later (in the buffer read by the previous round)
+            if (w >= g.wbeg[CCLS] && w - g.wbeg[CCLS] < g.ncitems && lane_id() == 0) {
+                const CItem ci = g.citems[w - g.wbeg[CCLS]];
+                if (ci.lead) g.bf[(seq + 2) % 3].flag[ci.node] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            if (!mk[j]) continue;
+            const int w = w0 + j * tw;
+            if (w >= g.wbeg[CCLS]) {
+                bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
+                continue;
+            }
+            switch (class_of_window(g, w)) {
+                case 0: bf_win<0, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
+                case 1: bf_win<1, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
+                case 2: bf_win<2, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
+                case 3: bf_win<3, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
+                default: bf_win<4, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
             }
         }
     }
@@ -1222,14 +1387,13 @@ struct EngineImpl {
     DBuf<unsigned char> sel_tmp;
     DBuf<HItem> hitems;
     DBuf<CItem> citems;
-    DBuf<long long> cmin;
-    DBuf<int> cunsat, carrive;
-    DBuf<int> hnchunks, harrive, hunsat;
-    DBuf<long long> hmin, inbox, part, flows;
+    DBuf<int> hnchunks, q_unsat, q_arrive;
+    DBuf<long long> q_req, q_taken, q_min, inbox, part, flows;
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
     DBuf<unsigned> trace;
+    DBuf<unsigned long long> stamps;
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;       // pinned host mirror
     long long* h_scr = nullptr; // pinned scratch: [0] eps
@@ -1250,9 +1414,9 @@ struct EngineImpl {
         rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release();
         dist.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
-        sel_tmp.release(); hitems.release(); citems.release(); cmin.release(); cunsat.release(); carrive.release(); hnchunks.release(); harrive.release(); hunsat.release();
-        hmin.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
-        ctr.release(); trace.release(); ctl.release();
+        sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release();
+        q_arrive.release(); q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
+        ctr.release(); trace.release(); stamps.release(); ctl.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
@@ -1285,14 +1449,13 @@ struct EngineImpl {
         g.nhitems = nhitems;
         g.citems = citems.p;
         g.ncitems = ncitems;
-        g.cmin = cmin.p;
-        g.cunsat = cunsat.p;
-        g.carrive = carrive.p;
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
-        g.harrive = harrive.p;
-        g.hmin = hmin.p;
-        g.hunsat = hunsat.p;
+        g.q_req = q_req.p;
+        g.q_taken = q_taken.p;
+        g.q_min = q_min.p;
+        g.q_unsat = q_unsat.p;
+        g.q_arrive = q_arrive.p;
         const int hs = std::max(1, nheavy);
         const size_t fs = std::max(1, hub_base);
         for (int k = 0; k < 6; ++k) {
@@ -1303,10 +1466,13 @@ struct EngineImpl {
         g.ctl = ctl.p;
         g.ctr = ctr.p;
         g.trace = trace.n > 1 ? trace.p : nullptr;
+        g.stamps = stamps.n > 1 ? stamps.p : nullptr;
+        g.stamp_sweep = -1;
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
-    int bf_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
+    int dense_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
+    int sparse_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB)); }
 };
 
 #define KS_CHECK(expr)                                                   \
@@ -1381,6 +1547,15 @@ int Engine::copy_to_device(void* dev_dst, const void* host_src, size_t bytes, st
         KS_CHECK(hipStreamSynchronize(s.stream));
     }
     return KS_OK;
+}
+
+// "index:path" → index, path
+static bool g_trace_ok(const char* spec, int& idx, std::string& path) {
+    const char* c = std::strchr(spec, ':');
+    if (!c) return false;
+    idx = std::atoi(spec);
+    path = c + 1;
+    return true;
 }
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -1554,21 +1729,14 @@ int Engine::solve(ks_result& res, std::string& err) {
         s.nhitems = (int)items.size();
         KS_CHECK(s.hitems.ensure(items.size()));
         KS_CHECK(s.hnchunks.ensure(s.nheavy));
-        KS_CHECK(s.harrive.ensure(s.nheavy));
-        KS_CHECK(s.hunsat.ensure(s.nheavy));
-        KS_CHECK(s.hmin.ensure(s.nheavy));
         KS_CHECK(s.inbox.ensure((size_t)s.nheavy * SHARDS));
         KS_CHECK(s.flags.ensure(6 * (size_t)std::max(1, s.hub_base)));
         KS_CHECK(s.hubflags.ensure(6 * (size_t)std::max(1, s.nheavy)));
         KS_CHECK(hipMemsetAsync(s.flags.p, 0, 6 * (size_t)std::max(1, s.hub_base), st));
         KS_CHECK(hipMemsetAsync(s.hubflags.p, 0, 6 * (size_t)std::max(1, s.nheavy) * sizeof(int), st));
         if (s.nheavy) {
-            std::vector<long long> hm(s.nheavy, INF64);
             KS_CHECK(hipMemcpyAsync(s.hitems.p, items.data(), items.size() * sizeof(HItem), hipMemcpyHostToDevice, st));
             KS_CHECK(hipMemcpyAsync(s.hnchunks.p, nch.data(), nch.size() * sizeof(int), hipMemcpyHostToDevice, st));
-            KS_CHECK(hipMemcpyAsync(s.hmin.p, hm.data(), hm.size() * sizeof(long long), hipMemcpyHostToDevice, st));
-            KS_CHECK(hipMemsetAsync(s.harrive.p, 0, s.nheavy * sizeof(int), st));
-            KS_CHECK(hipMemsetAsync(s.hunsat.p, 0, s.nheavy * sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.inbox.p, 0, (size_t)s.nheavy * SHARDS * sizeof(long long), st));
             KS_CHECK(hipStreamSynchronize(st));
         }
@@ -1589,29 +1757,42 @@ int Engine::solve(ks_result& res, std::string& err) {
         }
         s.ncitems = (int)ci.size();
         KS_CHECK(s.citems.ensure(std::max<size_t>(1, ci.size())));
-        KS_CHECK(s.cmin.ensure(std::max(1, cn)));
-        KS_CHECK(s.cunsat.ensure(std::max(1, cn)));
-        KS_CHECK(s.carrive.ensure(std::max(1, cn)));
         if (!ci.empty())
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
-        if (cn) {
-            std::vector<long long> cm(cn, INF64);
-            KS_CHECK(hipMemcpyAsync(s.cmin.p, cm.data(), cn * sizeof(long long), hipMemcpyHostToDevice, st));
-            KS_CHECK(hipMemsetAsync(s.cunsat.p, 0, cn * sizeof(int), st));
-            KS_CHECK(hipMemsetAsync(s.carrive.p, 0, cn * sizeof(int), st));
-            KS_CHECK(hipStreamSynchronize(st));
-        }
+        // claim slots: hubs, then chunked nodes
+        const int nq = std::max(1, s.nheavy + cn);
+        KS_CHECK(s.q_req.ensure(nq));
+        KS_CHECK(s.q_taken.ensure(nq));
+        KS_CHECK(s.q_min.ensure(nq));
+        KS_CHECK(s.q_unsat.ensure(nq));
+        KS_CHECK(s.q_arrive.ensure(nq));
+        std::vector<long long> qm(nq, INF64);
+        KS_CHECK(hipMemcpyAsync(s.q_min.p, qm.data(), nq * sizeof(long long), hipMemcpyHostToDevice, st));
+        KS_CHECK(hipMemsetAsync(s.q_req.p, 0, nq * sizeof(long long), st));
+        KS_CHECK(hipMemsetAsync(s.q_taken.p, 0, nq * sizeof(long long), st));
+        KS_CHECK(hipMemsetAsync(s.q_unsat.p, 0, nq * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.q_arrive.p, 0, nq * sizeof(int), st));
+        KS_CHECK(hipStreamSynchronize(st));
     }
     KS_CHECK(hipEventRecord(s.ev[1], st));
 
     // ------------------------------------------------------------ phases ---
+    const char* stamp_env = std::getenv("KS_STAMP");   // "sweep_index:path"
+    int stamp_at = -1;
+    std::string stamp_path;
+    if (stamp_env && *stamp_env && g_trace_ok(stamp_env, stamp_at, stamp_path)) {
+        KS_CHECK(s.stamps.ensure(3 * (size_t)(s.nhitems + s.ncitems / WPB + s.wbeg[NGC] / WPB + 64)));
+        KS_CHECK(hipMemsetAsync(s.stamps.p, 0, s.stamps.n * sizeof(unsigned long long), st));
+    }
     DG g = s.dg();
+    if (s.stamps.n > 1) g.stamp_sweep = stamp_at;
     {
         const char* ex = std::getenv("KS_EXPAND");
         g.expand = ex ? std::atoi(ex) : 0;
     }
-    const int fgrid = s.window_grid();
-    const int bgrid = s.bf_grid();
+    const int fgrid = s.window_grid();     // dense passes over every window (saturate)
+    const int dgrid = s.dense_grid();      // dense Bellman-Ford round
+    const int sgrid = s.sparse_grid();     // sparse sweeps and Bellman-Ford rounds
     const int ngrid = grid_for(nn, 2048);
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
@@ -1638,8 +1819,9 @@ int Engine::solve(ks_result& res, std::string& err) {
     auto bf_rounds = [&](bool pr, int k, bool first_dense) {
         for (int r = 0; r < k; ++r) {
             const int dense = (first_dense && r == 0) ? 1 : 0;
-            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(bgrid), dim3(BLK), 0, st, g, bseq, dense);
-            else hipLaunchKernelGGL(k_bf_round<false>, dim3(bgrid), dim3(BLK), 0, st, g, bseq, dense);
+            const int grid = dense ? dgrid : sgrid;
+            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
+            else hipLaunchKernelGGL(k_bf_round<false>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
             ++bseq;
             ++bf_launches;
         }
@@ -1692,7 +1874,7 @@ int Engine::solve(ks_result& res, std::string& err) {
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             for (int k = 0; k < gi; ++k) {
                 const long long ti = (long long)sweep_launches + k;
-                hipLaunchKernelGGL(k_sweep, dim3(bgrid), dim3(BLK), 0, st, g, k, sseq + k,
+                hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k, sseq + k,
                                    (g.trace && ti < kTraceMax) ? (int)ti : -1);
             }
             KS_CHECK(read_ctl());
@@ -1804,6 +1986,15 @@ int Engine::solve(ks_result& res, std::string& err) {
                 for (uint64_t i = 0; i < nt; ++i) std::fprintf(f, "%s%u", i ? ", " : "", ht[4 * i + k]);
             }
             std::fprintf(f, "]}\n");
+            std::fclose(f);
+        }
+    }
+    if (s.stamps.n > 1 && !stamp_path.empty()) {
+        std::vector<unsigned long long> hs(s.stamps.n);
+        KS_CHECK(hipMemcpy(hs.data(), s.stamps.p, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(stamp_path.c_str(), "w")) {
+            for (size_t b = 0; b + 2 < hs.size(); b += 3)
+                if (hs[b]) std::fprintf(f, "%zu %llu %llu %llu\n", b / 3, hs[b], hs[b + 1], hs[b + 2]);
             std::fclose(f);
         }
     }
