@@ -118,7 +118,7 @@ typedef struct ks_delta {
     int64_t  excess;           /* ADD_NODE, SET_EXCESS                                   */
 } ks_delta;
 
-#define KS_N_PHASE_TIMERS 6    /* build, refine, sweeps, global-update, verify, total    */
+#define KS_N_PHASE_TIMERS 6    /* build, saturate, cycles, price-refine, verify, total   */
 
 typedef struct ks_result {
     int64_t  total_cost;       /* Σ flow·cost over all arcs (lower bounds included)      */
@@ -131,15 +131,15 @@ typedef struct ks_result {
     uint64_t pushes;
     uint64_t relabels;
     uint64_t global_updates;
-    uint64_t gu_iterations;    /* Bellman-Ford relaxation rounds inside global updates   */
-    uint64_t gu_arc_scans;     /* residual-arc scans inside global updates               */
+    uint64_t gu_iterations;    /* Bellman-Ford rounds that did work (updates+refinement) */
+    uint64_t gu_arc_scans;     /* in-arc relaxations inside Bellman-Ford rounds          */
     double   ms_phase[KS_N_PHASE_TIMERS];
     int64_t  n_nodes;          /* node slots on device                                   */
     int64_t  n_arcs;           /* live input arcs                                        */
-    uint64_t sweep_launches;   /* k_sweep kernel launches (incl. early-exited ones)      */
-    double   ms_sweep_kernels; /* event-timed span of all sweep batches                   */
-    uint64_t gu_launches;      /* k_gu_relax kernel launches                              */
-    double   ms_gu_kernels;    /* event-timed span of all relaxation batches              */
+    uint64_t sweep_launches;   /* push/relabel sweep kernel launches (incl. early exits) */
+    double   ms_sweep_kernels; /* HIP-event-timed span of all sweep batches (ms)         */
+    uint64_t gu_launches;      /* Bellman-Ford round launches (price updates, refinement)*/
+    double   ms_gu_kernels;    /* HIP-event-timed span of all Bellman-Ford batches (ms)  */
 } ks_result;
 
 typedef struct ks_flow {       /* one "f src dst flow" line                              */

@@ -1368,6 +1368,7 @@ struct EngineImpl {
     ks_opts opts{};
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
+    hipEvent_t kev[4] = {};   // per-cycle kernel-batch timing: BF rounds, sweeps
 
     // input (compacted) graph, original ids
     int64_t n = 0, m = 0;
@@ -1420,6 +1421,8 @@ struct EngineImpl {
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : kev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1501,6 +1504,7 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     KS_CHECK(hipSetDevice(device));
     KS_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
+    for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
@@ -1799,8 +1803,11 @@ int Engine::solve(ks_result& res, std::string& err) {
     gi = std::max(2, std::min(MAXB, gi)) & ~1;     // even: sweeps end on p0
     const int pr_cap = 160;                        // price-refinement rounds before giving up
     const bool use_pr = s.opts.price_refine != 0;
+    long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
+    if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
     long long eps = std::max<long long>(1, (long long)s.maxc * mult);
-    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, cycles = 0;
+    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, cycles = 0, sweep_kernels = 0;
+    double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
     int phases = 0, pr_skips = 0;
     int kb = 24;                        // Bellman-Ford rounds enqueued per cycle (adaptive)
     int sseq = 0, bseq = 0;             // frontier buffer sequences
@@ -1834,9 +1841,12 @@ int Engine::solve(ks_result& res, std::string& err) {
         int used = 0, ok = 0;
         for (int batch = 0; used < pr_cap; ++batch) {
             const int k = std::min(64, pr_cap - used);
+            KS_CHECK(hipEventRecord(s.kev[0], st));
             bf_rounds(true, k, batch == 0);
+            KS_CHECK(hipEventRecord(s.kev[1], st));
             used += k;
             KS_CHECK(read_ctl());
+            ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
             if (s.h_ctl->bf_done) {
                 ok = 1;
                 break;
@@ -1869,16 +1879,23 @@ int Engine::solve(ks_result& res, std::string& err) {
                 hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g);
                 ptrace.back().gu_at.push_back(sweep_launches);
             }
+            KS_CHECK(hipEventRecord(s.kev[0], st));
             bf_rounds(false, kb, new_gu);
+            KS_CHECK(hipEventRecord(s.kev[1], st));
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
+            KS_CHECK(hipEventRecord(s.kev[2], st));
             for (int k = 0; k < gi; ++k) {
                 const long long ti = (long long)sweep_launches + k;
                 hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k, sseq + k,
                                    (g.trace && ti < kTraceMax) ? (int)ti : -1);
             }
+            KS_CHECK(hipEventRecord(s.kev[3], st));
             KS_CHECK(read_ctl());
             ++cycles;
+            sweep_kernels += gi;
+            ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
+            ms_sw_k += ev_ms(s.kev[2], s.kev[3]);
             if (s.h_ctl->infeasible) {
                 status = KS_E_INFEASIBLE;
                 break;
@@ -1918,7 +1935,7 @@ int Engine::solve(ks_result& res, std::string& err) {
         if (status) break;
         // certify optimality early: a flow that is 1-optimal (scaled) is optimal.
         // Tried once ε is below 1/32 of a cost unit, where it usually succeeds.
-        if (use_pr && eps > 1 && eps * 32 < mult) {
+        if (use_pr && eps > 1 && eps * pr_div < mult) {
             int used = 0;
             int rc = price_refine(1, &used);
             if (rc < 0) return rc;
@@ -2014,10 +2031,10 @@ int Engine::solve(ks_result& res, std::string& err) {
     res.ms_phase[4] = ev_ms(s.ev[6], s.ev[7]);
     res.ms_phase[5] = 1e3 * wall_s();
     res.gu_arc_scans = tc[C_GUSCAN];
-    res.sweep_launches = sweep_launches;
-    res.ms_sweep_kernels = ms_cycles;
+    res.sweep_launches = sweep_kernels;
+    res.ms_sweep_kernels = ms_sw_k;
     res.gu_launches = bf_launches;
-    res.ms_gu_kernels = ms_pr;
+    res.ms_gu_kernels = ms_bf_k;
     res.status = status;
     (void)pr_skips;
     (void)cycles;

@@ -49,7 +49,7 @@ class KsResult(C.Structure):
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ms_phase"}
-        names = ("build", "saturate", "sweeps", "global_update", "verify", "total")
+        names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d
 
