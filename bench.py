@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
-"""bench.py — MCMF solve latency and arcs/s on the Quincy-shaped config-3 cell
-graph (100k tasks × 10k machines), one full re-solve per step.
+"""bench.py — MCMF solve latency and arcs/s on Quincy-shaped cell graphs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload full|incremental|batch]
 
-N > 1 runs under torch.distributed (one rank per GPU, RCCL): every rank solves
-its own independent cell graph (seed + rank) — the north star's sharding of
-independent graphs — and the task→PU mappings are gathered to all ranks over
-RCCL after the timed region. `value` = Σ arcs over ranks ÷ max-rank time.
-Inputs are resident in HBM before timing (the first, untimed solve uploads);
-each timed step rebuilds the residual CSR on device and solves from scratch.
+* ``full`` (default, the headline line): config 3 (100k tasks × 10k machines),
+  one full device re-solve per step. N > 1 runs under torch.distributed (one
+  rank per GPU, RCCL): every rank solves its own independent cell graph
+  (seed + rank), the north star's sharding of independent graphs; the task→PU
+  mappings are gathered over RCCL after the timed region.
+  ``value`` = Σ arcs over ranks ÷ max-rank time.
+* ``incremental``: config 4 — the config-3 cell under churn (5% completions +
+  5% arrivals per round, pins, ageing, capacity refresh); a step is one round:
+  ks_apply_deltas + ks_solve + ks_get_task_mapping.
+* ``batch``: config 5 — 64 independent config-2 graphs (seeds 1000..1063)
+  round-robin over the ranks, solved concurrently per GPU (ks_solve_many); a
+  step solves every graph once. Mappings are gathered over RCCL afterwards.
+
+Inputs are resident in HBM before timing (the first, untimed solve uploads).
 """
 from __future__ import annotations
 
@@ -22,7 +29,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from ksched_amd import gen, native  # noqa: E402
+from ksched_amd import batch, churn, gen, native  # noqa: E402
 
 METRIC = "MCMF solve latency (ms) + arcs/s at 100k tasks x 10k machines, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
@@ -54,87 +61,99 @@ def roofline_of(results):
     return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
             "bytes_per_launch": round(b / max(1, n), 1), "avg_launch_us": round(1e3 * ms / max(1, n), 3),
-            "launches": n, "kernel_ms_per_step": round(ms / len(results), 3),
-            "other_kernel": {"k_sweep": {"ms_per_step": round(sw_ms / len(results), 3), "launches": sw_n,
+            "launches": n, "kernel_ms_per_step": round(ms / max(1, len(results)), 3),
+            "other_kernel": {"k_sweep": {"ms_per_step": round(sw_ms / max(1, len(results)), 3), "launches": sw_n,
                                          "bytes": sw_b},
-                             "k_bf_round": {"ms_per_step": round(bf_ms / len(results), 3), "launches": bf_n,
+                             "k_bf_round": {"ms_per_step": round(bf_ms / max(1, len(results)), 3), "launches": bf_n,
                                             "bytes": bf_b}}}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="config3", choices=sorted(gen.CONFIGS))
-    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--alpha", type=int, default=0)
-    ap.add_argument("--gu-interval", type=int, default=0)
-    ap.add_argument("--price-refine", type=int, default=-1)
-    args = ap.parse_args()
+class Dist:
+    """torch.distributed over RCCL when launched with WORLD_SIZE > 1."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = torch = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.dist, self.torch = dist, torch
 
-    T, M, R, J, seed = gen.CONFIGS[args.config]
-    g = gen.quincy(T, M, R, J, seed + rank)
-    opts = {}
+    def sync(self):
+        if self.dist:
+            self.torch.cuda.synchronize()
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def opts_of(args) -> dict:
+    o = {}
     if args.alpha:
-        opts["alpha"] = args.alpha
+        o["alpha"] = args.alpha
     if args.gu_interval:
-        opts["gu_interval"] = args.gu_interval
+        o["gu_interval"] = args.gu_interval
     if args.price_refine >= 0:
-        opts["price_refine"] = args.price_refine
-    ctx = native.Context(local, **opts)
-    ctx.load_graph(g)
+        o["price_refine"] = args.price_refine
+    return o
 
+
+def base_line(args, D, value, ms_per_step, config, **extra):
+    line = {"metric": METRIC, "value": round(value, 1), "unit": "arcs/s", "n_gpus": D.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic", "config": config}
+    line.update(extra)
+    return line
+
+
+# --------------------------------------------------------------------- full
+def run_full(args, D):
+    T, M, R, J, seed = gen.CONFIGS[args.config]
+    g = gen.quincy(T, M, R, J, seed + D.rank)
+    ctx = native.Context(D.local, **opts_of(args))
+    ctx.load_graph(g)
     for _ in range(args.warmup):
         ctx.solve()
-    if dist:
-        torch.cuda.synchronize()
-        dist.barrier()
+    D.sync()
     t0 = time.perf_counter()
     results, step_ms = [], []
     for _ in range(args.steps):
         ts = time.perf_counter()
         results.append(ctx.solve())
         step_ms.append(1e3 * (time.perf_counter() - ts))
-    if dist:
-        torch.cuda.synchronize()
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    D.sync()
+    elapsed = D.max(time.perf_counter() - t0)
     ms_per_step = 1e3 * elapsed / max(1, args.steps)
-    value = world * g.m / (ms_per_step / 1e3)
+    value = D.world * g.m / (ms_per_step / 1e3)
 
-    # RCCL gather of the task→PU mappings (int64 PU id per task, 0 = unscheduled)
     gather = None
-    if dist:
-        buf = torch.zeros(T, dtype=torch.int64, device="cuda")
+    if D.dist:       # RCCL gather of the task→PU mappings (int64 PU id per task, 0 = unscheduled)
+        torch = D.torch
+        buf = torch.zeros(1, T, dtype=torch.int64, device="cuda")
         tg0 = time.perf_counter()
         ctx.task_pu_device(buf.data_ptr(), T)
-        out = torch.zeros(world * T, dtype=torch.int64, device="cuda")
-        dist.all_gather_into_tensor(out, buf)
+        out = batch.gather(buf, D.world, D.dist)
         torch.cuda.synchronize()
         gather = {"ms": 1e3 * (time.perf_counter() - tg0), "bytes_per_rank": T * 8,
                   "scheduled": int((out > 0).sum().item())}
 
-    last = results[-1].raw
     costs = sorted({r.cost for r in results})
-    roofline = roofline_of(results)
     cpu = None
     parity = {"gpu_costs": costs, "flow": results[-1].flow}
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from oracle import ko
         t1 = time.perf_counter()
         st, ccost, cflow, nmap, ms = ko.reference_path(g)
@@ -151,22 +170,168 @@ def main():
                                            "cores": 1}}
         parity.update({"cpu_cost": ccost, "cpu_flow": cflow, "cs_cost": cs_cost,
                        "match": costs == [ccost] == [cs_cost] and results[-1].flow == cflow})
-
-    line = {"metric": METRIC, "value": round(value, 1), "unit": "arcs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": f"{args.config}: Quincy-shaped cell graph T={T} M={M} R={R} J={J} "
-                                   f"(n={g.n}, m={g.m}), full device re-solve per step, one graph per GPU",
-                       "tasks": T, "machines": M, "racks": R, "jobs": J, "seed": seed, "n": g.n, "m": g.m,
-                       "parallelism": f"independent graphs x{world}"},
-            "step_ms": [round(x, 2) for x in step_ms],
-            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "gather": gather,
-            "solve": {k: v for k, v in last.items()}}
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    config = {"workload": f"{args.config}: Quincy-shaped cell graph T={T} M={M} R={R} J={J} "
+                          f"(n={g.n}, m={g.m}), full device re-solve per step, one graph per GPU",
+              "tasks": T, "machines": M, "racks": R, "jobs": J, "seed": seed, "n": g.n, "m": g.m,
+              "parallelism": f"independent graphs x{D.world}"}
+    line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
+                     roofline=roofline_of(results), cpu_baseline=cpu, parity=parity, gather=gather,
+                     solve=dict(results[-1].raw))
     ctx.close()
-    if dist:
-        dist.destroy_process_group()
+    return line
+
+
+# -------------------------------------------------------------- incremental
+def run_incremental(args, D):
+    T, M, R, J, seed = gen.CONFIGS["config3"]
+    cell = churn.Cell(T, M, R, J, seed + D.rank)
+    ctx = native.Context(D.local, **opts_of(args))
+    ctx.load_graph(cell.graph())
+    r0 = ctx.solve()
+    mp = ctx.task_mapping()
+    done = arrive = T // 20
+    rounds = []
+    results = []
+    t_total = 0.0
+    for i in range(args.warmup + args.steps):
+        d = cell.step(mp, done=done, arrive=arrive)
+        D.sync()
+        ts = time.perf_counter()
+        ctx.apply_deltas(d)
+        ta = time.perf_counter()
+        r = ctx.solve()
+        tb = time.perf_counter()
+        mp = ctx.task_mapping()
+        te = time.perf_counter()
+        D.sync()
+        dt = D.max(time.perf_counter() - ts)
+        rec = {"round": i + 1, "deltas": int(d.shape[0]), "ms": round(1e3 * dt, 3),
+               "apply_ms": round(1e3 * (ta - ts), 3), "solve_ms": round(1e3 * (tb - ta), 3),
+               "mapping_ms": round(1e3 * (te - tb), 3), "cost": r.cost, "flow": r.flow,
+               "m": r.raw["n_arcs"], "running": int((cell.state == cell.RUN).sum())}
+        if i >= args.warmup:
+            t_total += dt
+            results.append(r)
+        rounds.append(rec)
+    ms_per_step = 1e3 * t_total / max(1, args.steps)
+    m_avg = sum(r.raw["n_arcs"] for r in results) / max(1, len(results))
+    value = D.world * m_avg / (ms_per_step / 1e3)
+    parity = None
+    cpu = None
+    if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
+        from oracle import ko
+        g = cell.graph()
+        t1 = time.perf_counter()
+        st, ccost, cflow, _, ms = ko.reference_path(g)
+        dt = time.perf_counter() - t1
+        cpu = {"value": round(g.m / dt, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
+               "sample": f"one reference-path solve (export -> SSP -> f lines -> BFS) of the last round's "
+                         f"full graph, {dt:.1f} s single-threaded", "ms": round(1e3 * dt, 1)}
+        parity = {"last_round_gpu_cost": rounds[-1]["cost"], "cpu_cost": ccost, "cpu_flow": cflow,
+                  "match": rounds[-1]["cost"] == ccost and rounds[-1]["flow"] == cflow}
+    config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
+                          f"{arrive} arrivals per round, pins/ageing/capacity deltas; step = apply deltas + "
+                          f"re-solve + mapping", "tasks": T, "machines": M, "seed": seed,
+              "initial_solve_ms": round(r0.raw["ms"]["total"], 3), "parallelism": f"independent cells x{D.world}"}
+    line = base_line(args, D, value, ms_per_step, config, rounds=rounds, roofline=roofline_of(results),
+                     cpu_baseline=cpu, parity=parity)
+    ctx.close()
+    return line
+
+
+# -------------------------------------------------------------------- batch
+def run_batch(args, D):
+    T, M, R, J, _ = gen.CONFIGS["config2"]
+    num = args.graphs
+    mine = batch.assign(num, D.world, D.rank)
+    graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in mine]
+    ctxs = [native.Context(D.local, **opts_of(args)) for _ in graphs]
+    for c, g in zip(ctxs, graphs):
+        c.load_graph(g)
+    for _ in range(args.warmup):
+        native.solve_many(ctxs, workers=args.workers)
+    D.sync()
+    t0 = time.perf_counter()
+    results = []
+    step_ms = []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        results.extend(native.solve_many(ctxs, workers=args.workers))
+        step_ms.append(1e3 * (time.perf_counter() - ts))
+    D.sync()
+    elapsed = D.max(time.perf_counter() - t0)
+    ms_per_step = 1e3 * elapsed / max(1, args.steps)
+    arcs_all = num * gen.quincy_sizes(T, M, R, J)[1]
+    value = arcs_all / (ms_per_step / 1e3)
+
+    gather = None
+    try:
+        import torch
+        if torch.cuda.is_available():
+            slots = batch.slots_per_rank(num, D.world)
+            buf = torch.zeros(slots, T, dtype=torch.int64, device=f"cuda:{D.local}")
+            tg0 = time.perf_counter()
+            for i, c in enumerate(ctxs):
+                c.task_pu_device(buf[i].data_ptr(), T)
+            if D.dist:
+                full = batch.gather(buf, num, D.dist)
+            else:
+                full = buf[:num]
+            torch.cuda.synchronize()
+            gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
+                      "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
+    except ImportError:
+        pass
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import ko
+        k = min(num, 16)
+        sample = [gen.quincy(T, M, R, J, 1000 + i) for i in range(k)]
+        cores = min(16, os.cpu_count() or 1, k)
+        t1 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            outs = list(ex.map(ko.reference_path, sample))
+        dt = time.perf_counter() - t1
+        m2 = gen.quincy_sizes(T, M, R, J)[1]
+        cpu = {"value": round(k * m2 / dt, 1), "unit": "arcs/s", "cores": cores, "kind": "port",
+               "sample": f"reference path (export -> SSP -> f lines -> BFS) on the first {k} of the {num} graphs, "
+                         f"one graph per thread on {cores} threads, {dt:.2f} s",
+               "match": all(o[1] == r.cost for o, r in zip(outs, results[:k])) if D.world == 1 else None}
+    config = {"workload": f"config5: {num} independent config-2 graphs (T={T} M={M}, seeds 1000..{999 + num}) "
+                          f"round-robin over {D.world} GPU(s), solved concurrently ({args.workers} workers/GPU); "
+                          f"step = every graph solved once", "graphs": num, "tasks": T, "machines": M,
+              "graphs_per_gpu": len(mine), "parallelism": f"graph sharding x{D.world}"}
+    line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
+                     per_graph_ms=round(sum(r.raw["ms"]["total"] for r in results) / max(1, len(results)), 3),
+                     roofline=roofline_of(results), cpu_baseline=cpu, gather=gather)
+    for c in ctxs:
+        c.close()
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="full", choices=["full", "incremental", "batch"])
+    ap.add_argument("--config", default="config3", choices=sorted(gen.CONFIGS))
+    ap.add_argument("--graphs", type=int, default=64)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--alpha", type=int, default=0)
+    ap.add_argument("--gu-interval", type=int, default=0)
+    ap.add_argument("--price-refine", type=int, default=-1)
+    args = ap.parse_args()
+
+    D = Dist()
+    run = {"full": run_full, "incremental": run_incremental, "batch": run_batch}[args.workload]
+    line = run(args, D)
+    if D.rank == 0:
+        print(json.dumps(line), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

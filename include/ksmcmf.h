@@ -163,6 +163,15 @@ int ks_apply_deltas(ks_ctx* ctx, const ks_delta* deltas, size_t k);
 /* Solve min-cost flow on the current graph. result may be NULL. */
 int ks_solve(ks_ctx* ctx, ks_result* result);
 
+/* Solve k independent contexts concurrently (config 5: cluster cells /
+ * what-if graphs). `workers` host threads (0 = min(k, 4)) each take the next
+ * unsolved context and call ks_solve on it; contexts on one device run on
+ * their own streams and overlap on the GPU. results[i] (may be NULL) receives
+ * context i's result. Returns KS_OK, or the status of the first failing
+ * context in index order (the others still ran). No reference counterpart:
+ * ksched solves one graph per round (flowscheduler/scheduler.go:350). */
+int ks_solve_many(ks_ctx* const* ctxs, size_t k, int workers, ks_result* results);
+
 /* Arcs with positive flow from the last solve (the "f" lines). */
 int ks_get_flows(ks_ctx* ctx, ks_flow* out, size_t cap, size_t* count);
 

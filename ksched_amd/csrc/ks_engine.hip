@@ -176,7 +176,12 @@ __device__ __forceinline__ long long atom_min_ret(long long* p, long long v) {
 __device__ __forceinline__ void atom_min(long long* p, long long v) {
     __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ long long atom_load(long long* p) {
+// excess and dist are only ever changed by atomics (performed beyond the issuing
+// XCD's L2). Every load of them that hands data across workgroups or kernels is
+// an agent-scope load: a plain load can hit a stale copy in another XCD's L2
+// when a node's owner moves to a different XCD between launches (observed when
+// several solves share the GPU: over-pushes, lost distance updates).
+__device__ __forceinline__ long long atom_load(const long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -637,7 +642,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         if (pushed) atom_add(&g.excess[v], -pushed);
         long long np = pv;
         if (rem > 0) {
-            if (minc >= INF64) g.ctl->infeasible = 1;
+            if (minc >= INF64) atomicOr(&g.ctl->infeasible, 1);
             else np = pv - (minc + eps);
             c.relabel++;
             nf.flag[v] = 1;   // still active next sweep
@@ -682,7 +687,7 @@ __device__ __forceinline__ void settle(const DG& g, const Front& F, const Front&
     const long long now = atom_load(&g.excess[x]);
     long long np = px;
     if (!unsat && now > 0) {
-        if (mn >= INF64) g.ctl->infeasible = 1;
+        if (mn >= INF64) atomicOr(&g.ctl->infeasible, hub ? 2 : 4);
         else np = px - (mn + eps);
         c.relabel++;
     }
@@ -701,7 +706,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
     __shared__ long long s_take;
     const int x = it.node;
     const long long px = P[x];
-    const long long E = g.excess[x];
+    const long long E = atom_load(&g.excess[x]);
     long long r[PER_T], cr[PER_T], adm[PER_T];
     int w[PER_T];
     long long mine = 0;
@@ -764,7 +769,7 @@ __device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, con
     const int lane = lane_id();
     const int x = ci.node;
     const long long px = P[x];
-    const long long E = g.excess[x];
+    const long long E = atom_load(&g.excess[x]);
     const int a = ci.begin + lane;
     long long r = 0, cr = 0;
     int w = 0;
@@ -846,7 +851,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         long long e = 0, pv = 0;
         int b0 = 0, en = 0;
         if (v >= 0) {
-            e = g.excess[v];
+            e = atom_load(&g.excess[v]);
             pv = P[v];
             b0 = g.first[v];
             en = g.first[v + 1];
@@ -1031,7 +1036,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         long long d = INF64, pv = 0;
         int b0 = 0, en = 0;
         if (v >= 0) {
-            d = g.dist[v];
+            d = atom_load(&g.dist[v]);
             pv = g.p0[v];
             b0 = g.first[v];
             en = g.first[v + 1];
@@ -1045,7 +1050,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
 template <bool PR>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
                                          long long* hub_min, int& out, long long& scans) {
-    const long long dv = g.dist[ci.node];
+    const long long dv = atom_load(&g.dist[ci.node]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
@@ -1059,7 +1064,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
     long long dv = INF64;
-    if (v >= 0) dv = g.dist[v];
+    if (v >= 0) dv = atom_load(&g.dist[v]);
     const bool act = v >= 0 && (PR || dv < INF64);
     long long pv = 0;
     int b0 = 0, en = 0;
@@ -1194,16 +1199,11 @@ __global__ void k_gu_init(DG g) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
         g.ctl->gu_L = 0;
-        g.ctl->bfa[0] = g.ctl->bfa[1] = g.ctl->bfa[2] = 0;
+        for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        long long e;
-        if (v >= g.hub_base) {
-            drain_inbox(g, (int)v - g.hub_base);
-            e = atom_load(&g.excess[v]);
-        } else {
-            e = g.excess[v];
-        }
+        if (v >= g.hub_base) drain_inbox(g, (int)v - g.hub_base);
+        const long long e = atom_load(&g.excess[v]);
         g.dist[v] = e < 0 ? 0 : INF64;
     }
 }
@@ -1213,7 +1213,7 @@ __global__ void k_pr_init(DG g) {
     clear_fronts(g, g.bf);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
-        g.ctl->bfa[0] = g.ctl->bfa[1] = g.ctl->bfa[2] = 0;
+        for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
         g.dist[v] = 0;
@@ -1231,7 +1231,7 @@ __global__ void k_gu_max(DG g) {
     if (!g.ctl->bf_done) return;
     long long mx = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long d = g.dist[v];
+        const long long d = atom_load(&g.dist[v]);
         if (d < INF64) mx = max(mx, d);
     }
     mx = wave_max(mx);
@@ -1255,9 +1255,9 @@ __global__ void k_gu_apply(DG g, int sseq) {
     const Front F = g.sf[sseq % 3];
     int out = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long d = g.dist[v];
-        const long long e = g.excess[v];
-        if (d >= INF64 && e > 0) g.ctl->infeasible = 1;
+        const long long d = atom_load(&g.dist[v]);
+        const long long e = atom_load(&g.excess[v]);
+        if (d >= INF64 && e > 0) atomicOr(&g.ctl->infeasible, 8);
         const long long dd = d < L ? d : L;
         const long long np = g.p0[v] - eps * dd;
         g.p0[v] = np;
@@ -1272,7 +1272,7 @@ __global__ void k_pr_apply(DG g) {
     if (!g.ctl->bf_done) return;
     const long long eps = g.ctl->eps;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long np = g.p0[v] - eps * g.dist[v];
+        const long long np = g.p0[v] - eps * atom_load(&g.dist[v]);
         g.p0[v] = np;
         g.p1[v] = np;
     }
@@ -1329,7 +1329,7 @@ __global__ void k_verify_opt(DG g, long long m2) {
 __global__ void k_verify_nodes(DG g) {
     int bad = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
-        if (g.excess[v] != 0) bad = 1;
+        if (atom_load(&g.excess[v]) != 0) bad = 1;
     if (__any(bad) && lane_id() == 0) atomicOr(&g.ctl->verify_bad, 4);
 }
 
@@ -1947,7 +1947,10 @@ int Engine::solve(ks_result& res, std::string& err) {
         }
     } while (eps > 1);
 
-    if (status == KS_E_INFEASIBLE) err = "infeasible: some supply cannot reach a demand node";
+    if (status == KS_E_INFEASIBLE)
+        err = "infeasible: some supply cannot reach a demand node (code " + std::to_string(s.h_ctl->infeasible) +
+              ", phase " + std::to_string(phases) + ", eps " + std::to_string(eps) + ", updates " +
+              std::to_string(gus) + ", sweeps " + std::to_string(sweep_launches) + ")";
 
     // ------------------------------------------------------------ verify ---
     KS_CHECK(hipEventRecord(s.ev[6], st));

@@ -11,10 +11,12 @@
 // NodeIDs index node slots directly, at most one arc per (src, dst), REMOVE_NODE
 // drops incident arcs. The device engine (ks_engine.hip) solves the compacted graph.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -371,6 +373,26 @@ int ks_solve(ks_ctx* c, ks_result* out) {
     r.status = rc;
     if (out) *out = r;
     return rc;
+}
+
+int ks_solve_many(ks_ctx* const* ctxs, size_t k, int workers, ks_result* results) {
+    if (k && !ctxs) return KS_E_INVALID;
+    for (size_t i = 0; i < k; ++i)
+        if (!ctxs[i]) return KS_E_INVALID;
+    std::vector<int> rcs(k, KS_OK);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < k;) rcs[i] = ks_solve(ctxs[i], results ? &results[i] : nullptr);
+    };
+    size_t nw = workers > 0 ? (size_t)workers : 4;
+    nw = std::min(nw, k);
+    std::vector<std::thread> pool;
+    for (size_t w = 1; w < nw; ++w) pool.emplace_back(work);
+    if (nw) work();
+    for (auto& t : pool) t.join();
+    for (int rc : rcs)
+        if (rc != KS_OK) return rc;
+    return KS_OK;
 }
 
 int ks_get_flows(ks_ctx* c, ks_flow* out, size_t cap, size_t* count) {

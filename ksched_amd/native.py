@@ -18,7 +18,7 @@ KS_ADD_NODE, KS_REMOVE_NODE, KS_ADD_ARC, KS_UPDATE_ARC, KS_SET_EXCESS = 0, 1, 2,
 
 EXPORTED_SYMBOLS = (
     "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
-    "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device",
+    "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
 )
 
 NODE_DT = np.dtype({"names": ["id", "excess", "type", "_pad"],
@@ -77,6 +77,14 @@ def load(build_if_missing: bool = True):
         if not build_if_missing:
             raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
         _build.build()
+    if os.environ.get("KS_PRELOAD_TORCH", "1") != "0":
+        # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7) and links it by file name, so if the library loaded
+        # /opt/rocm's copy first, a later torch.cuda init would bring up a second
+        # HIP/HSA runtime and fail ("No HIP GPUs are available"). Importing torch
+        # first makes libksmcmf bind to the runtime already loaded (same SONAME),
+        # so the RCCL gather and the solver share device pointers and streams.
+        import torch  # noqa: F401
     L = C.CDLL(path)
     P, V = C.POINTER, C.c_void_p
     L.ks_abi_version.restype = C.c_int
@@ -92,6 +100,7 @@ def load(build_if_missing: bool = True):
     L.ks_get_flows.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_task_mapping.argtypes = [V, V, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_task_pu_device.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
+    L.ks_solve_many.argtypes = [P(V), C.c_size_t, C.c_int, P(KsResult)]
     _LIB = L
     return L
 
@@ -192,3 +201,17 @@ class Context:
         cnt = C.c_size_t()
         self._check(self._L.ks_get_task_pu_device(self._h, C.c_void_p(dev_ptr), cap, C.byref(cnt)))
         return cnt.value
+
+
+def solve_many(ctxs: list[Context], workers: int = 0) -> list[SolveResult]:
+    """ks_solve_many: solve independent contexts concurrently (native worker
+    threads, one stream per context). Raises KsError on the first failure."""
+    L = load()
+    k = len(ctxs)
+    hs = (C.c_void_p * max(1, k))(*[c._h for c in ctxs])
+    rs = (KsResult * max(1, k))()
+    rc = L.ks_solve_many(hs, k, workers, rs)
+    if rc != KS_OK:
+        bad = next(c for c, r in zip(ctxs, rs) if r.status != KS_OK)
+        bad._check(rc)
+    return [SolveResult(r.total_cost, r.flow_value, r.as_dict()) for r in rs[:k]]

@@ -19,6 +19,75 @@ def graph_from_lists(nodes, arcs):
                      a[:, 4].copy())
 
 
+def flow_mapping(g, flow) -> dict[int, int]:
+    """task → last PU on its unit's path, following positive-flow arcs (the
+    scheduling network is a DAG); the test-side twin of ks_get_task_mapping."""
+    out = {}
+    pos = np.nonzero(np.asarray(flow) > 0)[0]
+    nxt: dict[int, list] = {}
+    for i in pos.tolist():
+        nxt.setdefault(int(g.src[i]), []).append([int(g.dst[i]), int(flow[i])])
+    for t in (np.nonzero(g.ntype == 1)[0] + 1).tolist():
+        v, last = t, None
+        for _ in range(g.n + 1):
+            if g.ntype[v - 1] == 2:
+                last = v
+            lst = nxt.get(v)
+            while lst and lst[0][1] == 0:
+                lst.pop(0)
+            if not lst:
+                break
+            lst[0][1] -= 1
+            v = lst[0][0]
+        if last is not None:
+            out[t] = last
+    return out
+
+
+def apply_deltas_to_arcs(nodes: dict, arcs: dict, deltas) -> None:
+    """Test-side restatement of the graph-store semantics of ks_apply_deltas
+    (include/ksmcmf.h): nodes {id: [excess, type]}, arcs {(s, d): (low, cap, cost)}."""
+    for x in deltas:
+        k = int(x["kind"])
+        if k == 0:
+            assert int(x["id"]) not in nodes
+            nodes[int(x["id"])] = [int(x["excess"]), int(x["type"])]
+        elif k == 1:
+            i = int(x["id"])
+            del nodes[i]
+            for key in [a for a in arcs if i in a]:
+                del arcs[key]
+        elif k == 2:
+            s, d = int(x["src"]), int(x["dst"])
+            assert s in nodes and d in nodes
+            arcs[(s, d)] = (int(x["low"]), int(x["cap"]), int(x["cost"]))
+        elif k == 3:
+            s, d = int(x["src"]), int(x["dst"])
+            if int(x["low"]) == 0 and int(x["cap"]) == 0:
+                arcs.pop((s, d), None)
+            else:
+                arcs[(s, d)] = (int(x["low"]), int(x["cap"]), int(x["cost"]))
+        else:
+            nodes[int(x["id"])][0] = int(x["excess"])
+
+
+def graph_from_store(nodes: dict, arcs: dict):
+    n = max(nodes) if nodes else 0
+    ntype = np.zeros(n, np.int32)
+    supply = np.zeros(n, np.int64)
+    for i, (e, t) in nodes.items():
+        ntype[i - 1] = t
+        supply[i - 1] = e
+    sink = np.nonzero(ntype == 3)[0]
+    if sink.shape[0] == 1:                  # auto_sink: the sink absorbs every other supply
+        supply[sink[0]] = 0
+        supply[sink[0]] = -int(supply.sum())
+    keys = sorted(arcs)
+    a = np.asarray([(s, d, *arcs[(s, d)]) for s, d in keys], np.int64).reshape(-1, 5)
+    return gen.Graph(ntype, supply, a[:, 0].copy(), a[:, 1].copy(), a[:, 2].copy(), a[:, 3].copy(),
+                     a[:, 4].copy())
+
+
 def random_graphs(seed: int, count: int, max_n: int = 60, cost_lo: int = 0, cost_hi: int = 100):
     """General digraphs (cycles, antiparallel arcs, zero capacities, some lower
     bounds) with a few random balanced supply/demand pairs; may be infeasible."""
