@@ -13,8 +13,10 @@
   5% arrivals per round, pins, ageing, capacity refresh); a step is one round:
   ks_apply_deltas + ks_solve + ks_get_task_mapping.
 * ``batch``: config 5 — 64 independent config-2 graphs (seeds 1000..1063)
-  round-robin over the ranks, solved concurrently per GPU (ks_solve_many); a
-  step solves every graph once. Mappings are gathered over RCCL afterwards.
+  round-robin over the ranks; each GPU solves its share as ONE device solve of
+  their disjoint union (``--batch-mode union``, default) or as concurrent
+  contexts (``--batch-mode streams``, ks_solve_many); a step solves every graph
+  once. Mappings are gathered over RCCL afterwards.
 
 Inputs are resident in HBM before timing (the first, untimed solve uploads).
 """
@@ -25,6 +27,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -111,6 +115,11 @@ def opts_of(args) -> dict:
     return o
 
 
+def full_opts(args) -> dict:
+    """Every timed full-workload step is a from-scratch solve: no warm start."""
+    return dict(opts_of(args), warm_start=0)
+
+
 def base_line(args, D, value, ms_per_step, config, **extra):
     line = {"metric": METRIC, "value": round(value, 1), "unit": "arcs/s", "n_gpus": D.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -123,7 +132,7 @@ def base_line(args, D, value, ms_per_step, config, **extra):
 def run_full(args, D):
     T, M, R, J, seed = gen.CONFIGS[args.config]
     g = gen.quincy(T, M, R, J, seed + D.rank)
-    ctx = native.Context(D.local, **opts_of(args))
+    ctx = native.Context(D.local, **full_opts(args))
     ctx.load_graph(g)
     for _ in range(args.warmup):
         ctx.solve()
@@ -185,7 +194,7 @@ def run_full(args, D):
 def run_incremental(args, D):
     T, M, R, J, seed = gen.CONFIGS["config3"]
     cell = churn.Cell(T, M, R, J, seed + D.rank)
-    ctx = native.Context(D.local, **opts_of(args))
+    ctx = native.Context(D.local, **dict(opts_of(args), warm_start=args.warm))
     ctx.load_graph(cell.graph())
     r0 = ctx.solve()
     mp = ctx.task_mapping()
@@ -208,6 +217,9 @@ def run_incremental(args, D):
         rec = {"round": i + 1, "deltas": int(d.shape[0]), "ms": round(1e3 * dt, 3),
                "apply_ms": round(1e3 * (ta - ts), 3), "solve_ms": round(1e3 * (tb - ta), 3),
                "mapping_ms": round(1e3 * (te - tb), 3), "cost": r.cost, "flow": r.flow,
+               "warm": r.raw["warm_started"], "phases": r.raw["phases"], "sweeps": r.raw["sweeps"],
+               "updates": r.raw["global_updates"], "bf_rounds": r.raw["gu_iterations"],
+               "solve_parts_ms": {k: round(v, 2) for k, v in r.raw["ms"].items()},
                "m": r.raw["n_arcs"], "running": int((cell.state == cell.RUN).sum())}
         if i >= args.warmup:
             t_total += dt
@@ -231,7 +243,7 @@ def run_incremental(args, D):
                   "match": rounds[-1]["cost"] == ccost and rounds[-1]["flow"] == cflow}
     config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
                           f"{arrive} arrivals per round, pins/ageing/capacity deltas; step = apply deltas + "
-                          f"re-solve + mapping", "tasks": T, "machines": M, "seed": seed,
+                          f"{'warm-started' if args.warm else 'from-scratch'} re-solve + mapping", "tasks": T, "machines": M, "seed": seed,
               "initial_solve_ms": round(r0.raw["ms"]["total"], 3), "parallelism": f"independent cells x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, rounds=rounds, roofline=roofline_of(results),
                      cpu_baseline=cpu, parity=parity)
@@ -245,18 +257,25 @@ def run_batch(args, D):
     num = args.graphs
     mine = batch.assign(num, D.world, D.rank)
     graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in mine]
-    ctxs = [native.Context(D.local, **opts_of(args)) for _ in graphs]
-    for c, g in zip(ctxs, graphs):
-        c.load_graph(g)
+    if args.batch_mode == "union":
+        u, noff, _ = batch.union(graphs)
+        ctxs = [native.Context(D.local, **full_opts(args))]
+        ctxs[0].load_graph(u)
+        solve = lambda: [ctxs[0].solve()]
+    else:
+        ctxs = [native.Context(D.local, **full_opts(args)) for _ in graphs]
+        for c, g in zip(ctxs, graphs):
+            c.load_graph(g)
+        solve = lambda: native.solve_many(ctxs, workers=args.workers)
     for _ in range(args.warmup):
-        native.solve_many(ctxs, workers=args.workers)
+        solve()
     D.sync()
     t0 = time.perf_counter()
     results = []
     step_ms = []
     for _ in range(args.steps):
         ts = time.perf_counter()
-        results.extend(native.solve_many(ctxs, workers=args.workers))
+        results.extend(solve())
         step_ms.append(1e3 * (time.perf_counter() - ts))
     D.sync()
     elapsed = D.max(time.perf_counter() - t0)
@@ -264,31 +283,38 @@ def run_batch(args, D):
     arcs_all = num * gen.quincy_sizes(T, M, R, J)[1]
     value = arcs_all / (ms_per_step / 1e3)
 
+    # task→PU mappings: device-resident [slots, T] block per rank (PU id local to its
+    # cell, 0 = unscheduled), all-gathered over RCCL after the timed region
     gather = None
-    try:
-        import torch
-        if torch.cuda.is_available():
-            slots = batch.slots_per_rank(num, D.world)
-            buf = torch.zeros(slots, T, dtype=torch.int64, device=f"cuda:{D.local}")
-            tg0 = time.perf_counter()
+    import torch
+    if torch.cuda.is_available():
+        slots = batch.slots_per_rank(num, D.world)
+        buf = torch.zeros(slots, T, dtype=torch.int64, device=f"cuda:{D.local}")
+        tg0 = time.perf_counter()
+        if args.batch_mode == "union":
+            ctxs[0].task_pu_device(buf.data_ptr(), len(mine) * T)
+            off = torch.as_tensor(noff[:len(mine)], device=buf.device).view(-1, 1)
+            part = buf[:len(mine)]
+            part.sub_(torch.where(part > 0, off, torch.zeros_like(off)))
+        else:
             for i, c in enumerate(ctxs):
                 c.task_pu_device(buf[i].data_ptr(), T)
-            if D.dist:
-                full = batch.gather(buf, num, D.dist)
-            else:
-                full = buf[:num]
-            torch.cuda.synchronize()
-            gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
-                      "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
-    except ImportError:
-        pass
+        full = batch.gather(buf, num, D.dist) if D.dist else buf[:num]
+        torch.cuda.synchronize()
+        gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
+                  "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
 
+    if args.batch_mode == "union":
+        per_graph = batch.split_costs(u, noff, ctxs[0].flows())
+    else:
+        per_graph = np.asarray([r.cost for r in results[-len(ctxs):]], np.int64)
     cpu = None
+    parity = {"total_cost": int(per_graph.sum())}
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from concurrent.futures import ThreadPoolExecutor
         from oracle import ko
         k = min(num, 16)
-        sample = [gen.quincy(T, M, R, J, 1000 + i) for i in range(k)]
+        sample = graphs[:k]
         cores = min(16, os.cpu_count() or 1, k)
         t1 = time.perf_counter()
         with ThreadPoolExecutor(cores) as ex:
@@ -297,15 +323,17 @@ def run_batch(args, D):
         m2 = gen.quincy_sizes(T, M, R, J)[1]
         cpu = {"value": round(k * m2 / dt, 1), "unit": "arcs/s", "cores": cores, "kind": "port",
                "sample": f"reference path (export -> SSP -> f lines -> BFS) on the first {k} of the {num} graphs, "
-                         f"one graph per thread on {cores} threads, {dt:.2f} s",
-               "match": all(o[1] == r.cost for o, r in zip(outs, results[:k])) if D.world == 1 else None}
+                         f"one graph per thread on {cores} threads, {dt:.2f} s"}
+        parity.update({"checked_graphs": k, "match": bool(all(o[1] == int(c) for o, c in zip(outs, per_graph[:k])))})
+    mode = ("one device solve of their disjoint union" if args.batch_mode == "union"
+            else f"one context each, solved concurrently ({args.workers} workers/GPU)")
     config = {"workload": f"config5: {num} independent config-2 graphs (T={T} M={M}, seeds 1000..{999 + num}) "
-                          f"round-robin over {D.world} GPU(s), solved concurrently ({args.workers} workers/GPU); "
-                          f"step = every graph solved once", "graphs": num, "tasks": T, "machines": M,
-              "graphs_per_gpu": len(mine), "parallelism": f"graph sharding x{D.world}"}
+                          f"round-robin over {D.world} GPU(s), {mode}; step = every graph solved once",
+              "graphs": num, "tasks": T, "machines": M, "graphs_per_gpu": len(mine), "mode": args.batch_mode,
+              "parallelism": f"graph sharding x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
-                     per_graph_ms=round(sum(r.raw["ms"]["total"] for r in results) / max(1, len(results)), 3),
-                     roofline=roofline_of(results), cpu_baseline=cpu, gather=gather)
+                     roofline=roofline_of(results), cpu_baseline=cpu, gather=gather, parity=parity,
+                     solve=dict(results[-1].raw))
     for c in ctxs:
         c.close()
     return line
@@ -320,6 +348,8 @@ def main():
     ap.add_argument("--config", default="config3", choices=sorted(gen.CONFIGS))
     ap.add_argument("--graphs", type=int, default=64)
     ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--batch-mode", default="union", choices=["union", "streams"])
+    ap.add_argument("--warm", type=int, default=1, help="incremental workload: warm-start re-solves")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--alpha", type=int, default=0)
     ap.add_argument("--gu-interval", type=int, default=0)

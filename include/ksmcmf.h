@@ -81,7 +81,9 @@ typedef struct ks_opts {
     int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */
     int32_t  price_refine;     /* certify optimality early by price refinement (1)      */
     int32_t  gu_interval;      /* sweeps between global price updates (default 32)      */
-    int32_t  reserved[11];
+    int32_t  warm_start;       /* re-solve from the previous flow and prices after
+                                  ks_apply_deltas (1); 0 = every solve from scratch    */
+    int32_t  reserved[10];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */
@@ -140,6 +142,8 @@ typedef struct ks_result {
     double   ms_sweep_kernels; /* HIP-event-timed span of all sweep batches (ms)         */
     uint64_t gu_launches;      /* Bellman-Ford round launches (price updates, refinement)*/
     double   ms_gu_kernels;    /* HIP-event-timed span of all Bellman-Ford batches (ms)  */
+    int32_t  warm_started;     /* 1 when this solve started from the previous solution   */
+    int32_t  reserved0;
 } ks_result;
 
 typedef struct ks_flow {       /* one "f src dst flow" line                              */

@@ -45,6 +45,42 @@ def pack(maps: list[np.ndarray], slots: int, tasks: int) -> np.ndarray:
     return out
 
 
+def union(graphs):
+    """Disjoint union of cell graphs as ONE flow network (node ids offset per
+    graph). The min-cost flow of a disjoint union is the union of the parts'
+    optima, so one device solve fills the GPU with every cell at once instead
+    of many small latency-bound solves. Returns (graph, node_offset[k+1],
+    arc_offset[k+1]); graph i owns ids node_offset[i]+1 .. node_offset[i+1]."""
+    from .gen import Graph
+
+    noff = np.zeros(len(graphs) + 1, np.int64)
+    aoff = np.zeros(len(graphs) + 1, np.int64)
+    for i, g in enumerate(graphs):
+        noff[i + 1] = noff[i] + g.n
+        aoff[i + 1] = aoff[i] + g.m
+    cat = lambda f: np.concatenate([f(g) for g in graphs]) if graphs else np.zeros(0, np.int64)
+    src = cat(lambda g: g.src) + np.repeat(noff[:-1], [g.m for g in graphs])
+    dst = cat(lambda g: g.dst) + np.repeat(noff[:-1], [g.m for g in graphs])
+    u = Graph(cat(lambda g: g.ntype).astype(np.int32), cat(lambda g: g.supply), src, dst,
+              cat(lambda g: g.low), cat(lambda g: g.cap), cat(lambda g: g.cost),
+              cat(lambda g: g.arc_types()).astype(np.int32))
+    return u, noff, aoff
+
+
+def split_costs(u, noff, flows) -> np.ndarray:
+    """Per-part total cost from the union's positive-flow records (ks_flow:
+    src, dst, flow), Σ flow·cost over each part's arcs."""
+    n = int(noff[-1]) + 1
+    key = u.src.astype(np.int64) * n + u.dst.astype(np.int64)
+    order = np.argsort(key, kind="stable")
+    fk = flows["src"].astype(np.int64) * n + flows["dst"].astype(np.int64)
+    idx = order[np.searchsorted(key, fk, sorter=order)]
+    part = np.searchsorted(noff, flows["src"].astype(np.int64), side="left") - 1
+    out = np.zeros(len(noff) - 1, np.int64)
+    np.add.at(out, part, flows["flow"].astype(np.int64) * u.cost[idx])
+    return out
+
+
 def gather(block, num_graphs: int, dist, group=None):
     """All-gather the per-rank ``[slots, tasks]`` blocks (a torch tensor on the
     collective's device) and return ``[num_graphs, tasks]`` ordered by graph id."""

@@ -27,14 +27,19 @@ public:
     int init(int device, const ks_opts& opts, std::string& err);
 
     // Copy a compacted graph (0-based node slots) into device input arrays.
-    // supply[n] is the node excess after any auto-sink adjustment.
+    // supply[n] is the node excess after any auto-sink adjustment. For a warm
+    // start, prev_idx[m] gives each arc's index in the previous upload (−1 = new)
+    // and fresh[n] marks node slots created since the previous solve; both may
+    // be null (no warm start for this graph).
     int upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
                const int64_t* low, const int64_t* cap, const int64_t* cost,
-               const int64_t* supply, std::string& err);
+               const int64_t* supply, const int32_t* prev_idx, const uint8_t* fresh,
+               std::string& err);
 
     // Build the residual CSR on device and run ε-scaling push-relabel to
     // optimality, then verify on device. Fills r (never NULL here).
-    int solve(ks_result& r, std::string& err);
+    // warm: start from the previous solution when one maps onto this graph.
+    int solve(ks_result& r, bool warm, std::string& err);
 
     // Flow on every input arc (input order) from the last successful solve.
     int download_flows(int64_t* flows, std::string& err);

@@ -521,7 +521,7 @@ struct ClassIs {
 // Push the full residual capacity of every arc with negative reduced cost
 // (Goldberg's refine start) over the whole graph; reads the authoritative p0.
 template <int G>
-__device__ __forceinline__ void sat_group(const DG& g, int v, Pend& pd, int& out, Cnt& c) {
+__device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pend& pd, int& out, Cnt& c) {
     const long long* P = g.p0;
     const int lig = lane_id() & (G - 1);
     int b0 = 0, en = 0;
@@ -539,7 +539,7 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, Pend& pd, int& out
             const long long r = g.rcap[a];
             if (r > 0) {
                 const int w = g.head[a];
-                if (g.cost[a] + pv - P[w] < 0) {
+                if (g.cost[a] + pv - P[w] < -thr) {
                     push_arc(g, nullptr, a, w, r, r, pd, out);
                     tot += r;
                     c.push++;
@@ -552,7 +552,9 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, Pend& pd, int& out
     if (v >= 0 && lig == 0 && tot) atom_add(&g.excess[v], -tot);
 }
 
-__global__ __launch_bounds__(BLK) void k_saturate(DG g) {
+// thr = 0: Goldberg's refine start (every negative reduced cost); thr = ε on a
+// warm start: only arcs that violate ε-optimality are saturated.
+__global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
     const long long* P = g.p0;
     Pend pd{-1, 0};
     Cnt c;
@@ -569,7 +571,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
                 const long long r = g.rcap[a];
                 if (r > 0) {
                     const int w = g.head[a];
-                    if (g.cost[a] + px - P[w] < 0) {
+                    if (g.cost[a] + px - P[w] < -thr) {
                         push_arc(g, nullptr, a, w, r, r, pd, out);
                         tot += r;
                         c.push++;
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g) {
         return;
     }
     const Scan sc{nullptr, 1};
-#define KS_SAT_CALL(C) sat_group<G_>(g, v, pd, out, c)
+#define KS_SAT_CALL(C) sat_group<G_>(g, v, thr, pd, out, c)
     KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SAT_CALL)
 #undef KS_SAT_CALL
     flush_pending(g, nullptr, pd, out);
@@ -1333,6 +1335,84 @@ __global__ void k_verify_nodes(DG g) {
     if (__any(bad) && lane_id() == 0) atomicOr(&g.ctl->verify_bad, 4);
 }
 
+// ======================================================== warm start ===
+// Incremental re-solve (config 4): the previous solve's flow on every arc that
+// survived the deltas (prev[i] = its index in the previous upload, −1 = new or
+// re-created; prev == nullptr: same arcs, same order) is re-applied, clamped
+// into the arc's current bounds; node imbalances become excess/deficit.
+__global__ void k_warm_flows(int m, const int* __restrict__ prev, const long long* __restrict__ pflows,
+                             const long long* __restrict__ low, const long long* __restrict__ cap,
+                             const int* __restrict__ fwd, const int* __restrict__ rev, long long* __restrict__ rcap,
+                             const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
+                             long long* __restrict__ excess) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
+        const int pi = prev ? prev[i] : (int)i;
+        if (pi < 0) continue;
+        const long long lo = low[i], c = cap[i];
+        long long f = pflows[pi];
+        f = (f < lo ? lo : (f > c ? c : f)) - lo;
+        if (f > 0) {
+            const int p = fwd[i];
+            rcap[p] = (c - lo) - f;
+            rcap[rev[p]] = f;
+            atom_add(&excess[perm[src[i]]], -f);
+            atom_add(&excess[perm[dst[i]]], f);
+        }
+    }
+}
+
+// Previous prices by node slot (ids are stable), rescaled when the cost
+// multiplier n+1 changed; slots beyond the previous graph start at 0.
+__global__ void k_warm_prices(int n, int n_prev, long long mult_prev, long long mult,
+                              const long long* __restrict__ pslot, const int* __restrict__ perm,
+                              long long* __restrict__ p0, long long* __restrict__ p1) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+        long long p = 0;
+        if (v < n_prev) {
+            const long long q = pslot[v];
+            p = mult == mult_prev ? q : (q / mult_prev) * mult + (q % mult_prev) * mult / mult_prev;
+        }
+        p0[perm[v]] = p;
+        p1[perm[v]] = p;
+    }
+}
+
+// Nodes created since the previous solve (fresh[v] = 1) get the lowest price
+// at which none of their residual out-arcs has a negative reduced cost.
+__global__ void k_fresh_prices(int n, const unsigned char* __restrict__ fresh, const int* __restrict__ perm,
+                               DG g) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+        if (!fresh[v]) continue;
+        const int x = perm[v];
+        long long best = -INF64;
+        for (int a = g.first[x]; a < g.first[x + 1]; ++a)
+            if (g.rcap[a] > 0) best = max(best, g.p0[g.head[a]] - g.cost[a]);
+        if (best > -INF64) {
+            g.p0[x] = best;
+            g.p1[x] = best;
+        }
+    }
+}
+
+// Largest ε-optimality violation −(c + p(u) − p(w)) over residual arcs → ctl->gu_L.
+__global__ void k_max_viol(DG g, long long m2) {
+    long long mx = 0;
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
+        if (g.rcap[p] > 0) {
+            const long long cr = g.cost[p] + g.p0[g.head[g.rev[p]]] - g.p0[g.head[p]];
+            if (-cr > mx) mx = -cr;
+        }
+    }
+    mx = wave_max(mx);
+    if (lane_id() == 0 && mx > 0) __hip_atomic_fetch_max(&g.ctl->gu_L, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_save_prices(int n, const int* __restrict__ perm, const long long* __restrict__ p0,
+                              long long* __restrict__ pslot) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
+        pslot[v] = p0[perm[v]];
+}
+
 // ============================================================ host helpers ===
 inline int grid_for(long long n, int cap = 4096) {
     long long b = (n + BLK - 1) / BLK;
@@ -1403,6 +1483,14 @@ struct EngineImpl {
     int hub_base = 0, nn = 0;   // grouped node ids [0, hub_base), hubs after: nn ids
     int obeg[NGC + 1] = {0}, oend[NGC] = {0}, wbeg[NGC + 1] = {0};
     bool solved = false;
+    // warm start: the last successful solve's flows (input order) and prices (by slot)
+    DBuf<int> a_prev;              // per input arc: index in the previous upload, −1 = new
+    DBuf<unsigned char> a_fresh;   // per node slot: created since the previous solve
+    DBuf<long long> prev_flows, p_slot;
+    bool has_prev = false, fresh_valid = false;
+    int map_state = 0;             // 0 no mapping, 1 same arcs as the last solve, 2 a_prev
+    int64_t n_prev = 0;
+    long long mult_prev = 1;
 
     ~EngineImpl() {
         if (stream) {
@@ -1418,6 +1506,7 @@ struct EngineImpl {
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release();
         q_arrive.release(); q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
         ctr.release(); trace.release(); stamps.release(); ctl.release();
+        a_prev.release(); a_fresh.release(); prev_flows.release(); p_slot.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
@@ -1513,7 +1602,8 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
 }
 
 int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int64_t* low,
-                   const int64_t* cap, const int64_t* cost, const int64_t* supply, std::string& err) {
+                   const int64_t* cap, const int64_t* cost, const int64_t* supply, const int32_t* prev_idx,
+                   const uint8_t* fresh, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
     if (n < 0 || m < 0 || n > (1LL << 28) || m > (1LL << 29)) {
@@ -1539,6 +1629,18 @@ int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
         KS_CHECK(hipMemcpyAsync(s.a_cost.p, cost, m * sizeof(long long), hipMemcpyHostToDevice, s.stream));
     }
     if (n) KS_CHECK(hipMemcpyAsync(s.supply.p, supply, n * sizeof(long long), hipMemcpyHostToDevice, s.stream));
+    s.map_state = 0;
+    s.fresh_valid = false;
+    if (prev_idx && s.has_prev) {
+        KS_CHECK(s.a_prev.ensure(m));
+        if (m) KS_CHECK(hipMemcpyAsync(s.a_prev.p, prev_idx, m * sizeof(int), hipMemcpyHostToDevice, s.stream));
+        s.map_state = 2;
+        if (fresh && n) {
+            KS_CHECK(s.a_fresh.ensure(n));
+            KS_CHECK(hipMemcpyAsync(s.a_fresh.p, fresh, n, hipMemcpyHostToDevice, s.stream));
+            s.fresh_valid = true;
+        }
+    }
     KS_CHECK(hipStreamSynchronize(s.stream));
     return KS_OK;
 }
@@ -1568,7 +1670,7 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
-int Engine::solve(ks_result& res, std::string& err) {
+int Engine::solve(ks_result& res, bool warm, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
     const auto t_host0 = std::chrono::steady_clock::now();
@@ -1577,7 +1679,14 @@ int Engine::solve(ks_result& res, std::string& err) {
     };
     hipStream_t st = s.stream;
     const int64_t n = s.n, m = s.m, m2 = 2 * m;
+    const bool use_warm = warm && s.has_prev && s.map_state != 0;
     s.solved = false;
+    s.has_prev = false;
+    if (use_warm) {   // the last solution becomes the warm-start input
+        std::swap(s.flows.p, s.prev_flows.p);
+        std::swap(s.flows.n, s.prev_flows.n);
+    }
+    res.warm_started = use_warm ? 1 : 0;
     res.n_nodes = n;
     res.n_arcs = m;
     if (n == 0) {
@@ -1834,13 +1943,13 @@ int Engine::solve(ks_result& res, std::string& err) {
         }
     };
     // Price refinement at eps_try: 1 = success (prices updated), 0 = failed, <0 error.
-    auto price_refine = [&](long long eps_try, int* rounds_used) -> int {
+    auto price_refine = [&](long long eps_try, int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(set_eps(eps_try));
         hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g);
         int used = 0, ok = 0;
-        for (int batch = 0; used < pr_cap; ++batch) {
-            const int k = std::min(64, pr_cap - used);
+        for (int batch = 0; used < cap; ++batch) {
+            const int k = std::min(64, cap - used);
             KS_CHECK(hipEventRecord(s.kev[0], st));
             bf_rounds(true, k, batch == 0);
             KS_CHECK(hipEventRecord(s.kev[1], st));
@@ -1860,13 +1969,39 @@ int Engine::solve(ks_result& res, std::string& err) {
         return ok;
     };
 
+    // warm start: previous flows and prices, then start at a small ε (≤ K cost
+    // units, K = KS_WARM_K, default 8) and saturate only the arcs that violate it
+    long long warm_thr = 0;
+    if (use_warm) {
+        const int wgrid = grid_for(m, 2048);
+        if (m)
+            hipLaunchKernelGGL(k_warm_flows, dim3(wgrid), dim3(BLK), 0, st, (int)m,
+                               s.map_state == 2 ? (const int*)s.a_prev.p : (const int*)nullptr,
+                               (const long long*)s.prev_flows.p, (const long long*)s.a_low.p,
+                               (const long long*)s.a_cap.p, (const int*)s.fwd.p, (const int*)s.rev.p, s.rcap.p,
+                               (const int*)s.a_src.p, (const int*)s.a_dst.p, (const int*)s.perm.p, s.excess.p);
+        hipLaunchKernelGGL(k_warm_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n, (int)s.n_prev,
+                           s.mult_prev, mult, (const long long*)s.p_slot.p, (const int*)s.perm.p, s.p0.p, s.p1.p);
+        if (s.fresh_valid && s.map_state == 2)
+            hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n,
+                               (const unsigned char*)s.a_fresh.p, (const int*)s.perm.p, g);
+        if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
+        KS_CHECK(read_ctl());
+        long long K = 8;
+        if (const char* wk = std::getenv("KS_WARM_K")) K = std::max(1LL, std::atoll(wk));
+        const long long viol = s.h_ctl->gu_L;
+        const long long e0 = std::max<long long>(1, std::min<long long>({viol, K * mult, eps}));
+        warm_thr = e0;
+        eps = e0 * alpha;   // the first phase runs at e0
+    }
+
     do {
         eps = std::max<long long>(1, eps / alpha);
         ++phases;
         ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}, 0});
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g);
+        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 ? warm_thr : 0LL);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         bool gu_running = false;
         uint64_t phase_sweeps = 0;
@@ -1937,7 +2072,7 @@ int Engine::solve(ks_result& res, std::string& err) {
         // Tried once ε is below 1/32 of a cost unit, where it usually succeeds.
         if (use_pr && eps > 1 && eps * pr_div < mult) {
             int used = 0;
-            int rc = price_refine(1, &used);
+            int rc = price_refine(1, &used, pr_cap);
             if (rc < 0) return rc;
             if (rc == 1) {
                 ++pr_skips;
@@ -2041,7 +2176,17 @@ int Engine::solve(ks_result& res, std::string& err) {
     res.status = status;
     (void)pr_skips;
     (void)cycles;
-    if (status == KS_OK) s.solved = true;
+    if (status == KS_OK) {
+        KS_CHECK(s.p_slot.ensure(n));
+        hipLaunchKernelGGL(k_save_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n, (const int*)s.perm.p,
+                           (const long long*)s.p0.p, s.p_slot.p);
+        KS_CHECK(hipStreamSynchronize(st));
+        s.solved = true;
+        s.has_prev = true;
+        s.map_state = 1;
+        s.n_prev = n;
+        s.mult_prev = mult;
+    }
     return status;
 }
 

@@ -29,6 +29,7 @@ struct NodeRec {
     int64_t excess = 0;
     int32_t type = 0;
     bool alive = false;
+    bool fresh = true;     // created since the last successful solve (warm start)
 };
 
 struct ArcRec {
@@ -36,6 +37,7 @@ struct ArcRec {
     int64_t low = 0, cap = 0, cost = 0;
     int32_t type = 0;
     bool alive = false;
+    int prev_up = -1;      // index in the last solved upload; −1 = new since (warm start)
 };
 
 constexpr uint64_t kMaxId = (1ULL << 30);
@@ -55,11 +57,14 @@ struct ks_ctx {
     std::unordered_map<uint64_t, int> arc_of;
     std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy)
     bool dirty = true;
+    bool reloaded = true;                  // ks_load_graph since the last solve: no warm start
 
     // last upload (compact arrays) and solve outputs
     std::vector<int> up_arc;               // compact index → arc slot
     std::vector<int32_t> c_src, c_dst;
     std::vector<int64_t> c_low, c_cap, c_cost, c_supply;
+    std::vector<int32_t> c_prev;
+    std::vector<uint8_t> c_fresh;
     std::vector<int64_t> flows;
     bool have_solution = false;
     bool flows_fresh = false;
@@ -86,6 +91,7 @@ void kill_arc(ks_ctx* c, int slot) {
     ArcRec& a = c->arcs[slot];
     if (!a.alive) return;
     a.alive = false;
+    a.prev_up = -1;
     c->arc_of.erase(arc_key(a.src, a.dst));
     c->free_arcs.push_back(slot);
 }
@@ -111,6 +117,7 @@ int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int6
             c->arcs.emplace_back();
         }
         c->arc_of.emplace(arc_key(s, d), slot);
+        c->arcs[slot].prev_up = -1;
         c->inc[s].push_back(slot);
         c->inc[d].push_back(slot);
     }
@@ -130,7 +137,7 @@ int add_node(ks_ctx* c, uint64_t id, int64_t excess, int32_t type) {
     ensure_node(c, id);
     if (c->nodes[id].alive)
         return c->fail(KS_E_INVALID, "node " + std::to_string(id) + " already present");  // graph.go:95-98
-    c->nodes[id] = NodeRec{excess, type, true};
+    c->nodes[id] = NodeRec{excess, type, true, true};
     return KS_OK;
 }
 
@@ -176,6 +183,8 @@ int upload(ks_ctx* c) {
     c->c_low.clear();
     c->c_cap.clear();
     c->c_cost.clear();
+    c->c_prev.clear();
+    const bool warm = c->opts.warm_start && !c->reloaded;
     for (int slot = 0; slot < (int)c->arcs.size(); ++slot) {
         const ArcRec& a = c->arcs[slot];
         if (!a.alive) continue;
@@ -185,10 +194,16 @@ int upload(ks_ctx* c) {
         c->c_low.push_back(a.low);
         c->c_cap.push_back(a.cap);
         c->c_cost.push_back(a.cost);
+        if (warm) c->c_prev.push_back(a.prev_up);
+    }
+    if (warm) {
+        c->c_fresh.assign(n, 0);
+        for (int64_t v = 0; v < n; ++v) c->c_fresh[v] = c->nodes[v + 1].alive && c->nodes[v + 1].fresh;
     }
     const int64_t m = (int64_t)c->up_arc.size();
     int rc = c->eng.upload(n, m, c->c_src.data(), c->c_dst.data(), c->c_low.data(), c->c_cap.data(),
-                           c->c_cost.data(), c->c_supply.data(), c->err);
+                           c->c_cost.data(), c->c_supply.data(), warm ? c->c_prev.data() : nullptr,
+                           warm ? c->c_fresh.data() : nullptr, c->err);
     if (rc == KS_OK) c->dirty = false;
     return rc;
 }
@@ -258,6 +273,7 @@ void ks_default_opts(ks_opts* o) {
     o->auto_sink = 1;
     o->price_refine = 1;
     o->gu_interval = 32;
+    o->warm_start = 1;
 }
 
 ks_ctx* ks_create(int device, const ks_opts* opts) {
@@ -291,6 +307,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     c->arcs.reserve(m);
     c->have_solution = false;
     c->dirty = true;
+    c->reloaded = true;
     for (size_t i = 0; i < n; ++i) {
         int rc = add_node(c, nodes[i].id, nodes[i].excess, nodes[i].type);
         if (rc) return rc;
@@ -362,8 +379,12 @@ int ks_solve(ks_ctx* c, ks_result* out) {
     c->flows_fresh = false;
     int rc = KS_OK;
     if (c->dirty) rc = upload(c);
-    if (rc == KS_OK) rc = c->eng.solve(r, c->err);
+    if (rc == KS_OK) rc = c->eng.solve(r, c->opts.warm_start != 0, c->err);
     if (rc == KS_OK) {
+        // remember which upload index every arc had, for the next warm start
+        for (size_t i = 0; i < c->up_arc.size(); ++i) c->arcs[c->up_arc[i]].prev_up = (int)i;
+        for (auto& nd : c->nodes) nd.fresh = false;
+        c->reloaded = false;
         int64_t pos = 0;
         for (int64_t v : c->c_supply)
             if (v > 0) pos += v;

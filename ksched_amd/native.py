@@ -35,7 +35,8 @@ FLOW_DT = np.dtype({"names": ["src", "dst", "flow"], "formats": ["<u8", "<u8", "
 
 class KsOpts(C.Structure):
     _fields_ = [("alpha", C.c_int32), ("verify", C.c_int32), ("auto_sink", C.c_int32),
-                ("price_refine", C.c_int32), ("gu_interval", C.c_int32), ("reserved", C.c_int32 * 11)]
+                ("price_refine", C.c_int32), ("gu_interval", C.c_int32), ("warm_start", C.c_int32),
+                ("reserved", C.c_int32 * 10)]
 
 
 class KsResult(C.Structure):
@@ -45,7 +46,8 @@ class KsResult(C.Structure):
                 ("global_updates", C.c_uint64), ("gu_iterations", C.c_uint64), ("gu_arc_scans", C.c_uint64),
                 ("ms_phase", C.c_double * 6), ("n_nodes", C.c_int64), ("n_arcs", C.c_int64),
                 ("sweep_launches", C.c_uint64), ("ms_sweep_kernels", C.c_double),
-                ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double)]
+                ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double), ("warm_started", C.c_int32),
+                ("reserved0", C.c_int32)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ms_phase"}

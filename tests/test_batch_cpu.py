@@ -54,3 +54,21 @@ def test_gloo_world2_gather(tmp_path):
     res = json.loads(out.read_text())
     assert res["ok"] and res["world"] == 2
     assert res["shape"] == [7, 150] and res["scheduled"] > 0
+
+
+def test_union_costs_split_per_graph():
+    """The disjoint union's optimum is the sum of the parts' optima, and the
+    per-part costs recovered from the union's flow records match each part."""
+    from ksched_amd import gen
+    from oracle import ko
+    graphs = [gen.quincy(200, 20, 2, 4, 50 + i) for i in range(4)]
+    u, noff, aoff = batch.union(graphs)
+    assert (u.n, u.m) == (sum(g.n for g in graphs), sum(g.m for g in graphs))
+    st, cost, flow, fl = ko.cost_scaling(u)
+    assert st == 0
+    parts = [ko.cost_scaling(g)[1] for g in graphs]
+    assert cost == sum(parts)
+    pos = np.nonzero(fl > 0)[0]
+    rec = np.zeros(pos.shape[0], [("src", "<u8"), ("dst", "<u8"), ("flow", "<i8")])
+    rec["src"], rec["dst"], rec["flow"] = u.src[pos], u.dst[pos], fl[pos]
+    assert batch.split_costs(u, noff, rec).tolist() == parts

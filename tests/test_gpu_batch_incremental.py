@@ -27,6 +27,7 @@ def test_incremental_rounds_match_full_resolve(ctx):
         st, cost, flow, _ = ko.cost_scaling(g)
         assert st == 0
         assert (r.cost, r.flow) == (cost, flow), f"round {rnd + 1}"
+        assert r.raw["warm_started"] == 1          # re-solved from the previous flow and prices
         fl = flows_by_arc(ctx, g)
         vst, vcost, _ = ko.verify(g, fl)
         assert vst == 0 and vcost == cost
@@ -65,3 +66,42 @@ def test_solve_many_matches_oracle():
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_union_batch_matches_parts(ctx):
+    """Config 5's union mode: one device solve of several cells; per-cell costs
+    from the flow records and per-cell mappings from the device vector."""
+    from ksched_amd import batch
+    T, M, R, J = 3_000, 300, 12, 30
+    graphs = [gen.quincy(T, M, R, J, 1100 + i) for i in range(5)]
+    u, noff, _ = batch.union(graphs)
+    ctx.load_graph(u)
+    r = ctx.solve()
+    parts = [ko.cost_scaling(g)[1] for g in graphs]
+    assert r.cost == sum(parts) and r.flow == 5 * T
+    assert batch.split_costs(u, noff, ctx.flows()).tolist() == parts
+    import torch
+    buf = torch.zeros(5, T, dtype=torch.int64, device="cuda")
+    assert ctx.task_pu_device(buf.data_ptr(), 5 * T) == 5 * T
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    for i, g in enumerate(graphs):
+        loc = np.where(host[i] > 0, host[i] - noff[i], 0)
+        mp = {int(t): int(p) for t, p in zip(np.nonzero(g.ntype == 1)[0] + 1, loc) if p > 0}
+        check_mapping(g, mp)
+
+
+def test_warm_resolve_without_changes_and_cold_opt_out():
+    g = gen.quincy(2_000, 200, 8, 20, 77)
+    st, cost, flow, _ = ko.cost_scaling(g)
+    with native.Context(0) as c:
+        c.load_graph(g)
+        r0 = c.solve()
+        r1 = c.solve()                           # same graph: warm identity start
+        assert (r0.cost, r1.cost) == (cost, cost)
+        assert r0.raw["warm_started"] == 0 and r1.raw["warm_started"] == 1
+    with native.Context(0, warm_start=0) as c:
+        c.load_graph(g)
+        c.solve()
+        r2 = c.solve()
+        assert r2.cost == cost and r2.raw["warm_started"] == 0
