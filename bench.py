@@ -349,7 +349,7 @@ def main():
     ap.add_argument("--graphs", type=int, default=64)
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--batch-mode", default="union", choices=["union", "streams"])
-    ap.add_argument("--warm", type=int, default=1, help="incremental workload: warm-start re-solves")
+    ap.add_argument("--warm", type=int, default=0, help="incremental workload: warm-start re-solves")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--alpha", type=int, default=0)
     ap.add_argument("--gu-interval", type=int, default=0)

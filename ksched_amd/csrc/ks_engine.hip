@@ -1900,16 +1900,22 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     DG g = s.dg();
     if (s.stamps.n > 1) g.stamp_sweep = stamp_at;
     {
-        const char* ex = std::getenv("KS_EXPAND");
-        g.expand = ex ? std::atoi(ex) : 0;
+        const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
+        g.expand = ex ? std::atoi(ex) : 1;
     }
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
     const int sgrid = s.sparse_grid();     // sparse sweeps and Bellman-Ford rounds
     const int ngrid = grid_for(nn, 2048);
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
-    int gi = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
-    gi = std::max(2, std::min(MAXB, gi)) & ~1;     // even: sweeps end on p0
+    int gi_base = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
+    gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
+    int gi_tail = 0;
+    long long tail_units = 1;
+    if (const char* e = std::getenv("KS_GI_TAIL")) gi_tail = std::max(2, std::min(MAXB, std::atoi(e))) & ~1;
+    if (const char* e = std::getenv("KS_GI_TAIL_UNITS")) tail_units = std::max(1LL, std::atoll(e));
+    int sat_eps = 0;   // KS_SAT_EPS=1: phase start saturates only arcs violating the new ε
+    if (const char* e = std::getenv("KS_SAT_EPS")) sat_eps = std::atoi(e);
     const int pr_cap = 160;                        // price-refinement rounds before giving up
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
@@ -1988,9 +1994,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         KS_CHECK(read_ctl());
         long long K = 8;
+        long long D = 1;   // KS_WARM_D: start below one cost unit (K·mult / D)
         if (const char* wk = std::getenv("KS_WARM_K")) K = std::max(1LL, std::atoll(wk));
+        if (const char* wd = std::getenv("KS_WARM_D")) D = std::max(1LL, std::atoll(wd));
         const long long viol = s.h_ctl->gu_L;
-        const long long e0 = std::max<long long>(1, std::min<long long>({viol, K * mult, eps}));
+        const long long e0 = std::max<long long>(1, std::min<long long>({viol, K * mult / D, eps}));
         warm_thr = e0;
         eps = e0 * alpha;   // the first phase runs at e0
     }
@@ -2001,10 +2009,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}, 0});
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 ? warm_thr : 0LL);
+        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g,
+                           phases == 1 && use_warm ? warm_thr : (sat_eps ? eps : 0LL));
         KS_CHECK(hipEventRecord(s.ev[3], st));
         bool gu_running = false;
         uint64_t phase_sweeps = 0;
+        // sweeps per update: gi, or gi_tail once ε is below tail_units cost units
+        const int gi = (gi_tail > 0 && eps < tail_units * mult) ? gi_tail : gi_base;
         int gu_r0 = 0;   // bf_count when the running update started
         for (;;) {
             // one cycle: [GU init] [kb BF rounds] [max] [apply] [gi sweeps]

@@ -17,7 +17,6 @@
 #include <new>
 #include <string>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/ksmcmf.h"
@@ -44,6 +43,84 @@ constexpr uint64_t kMaxId = (1ULL << 30);
 
 inline uint64_t arc_key(uint64_t s, uint64_t d) { return (s << 32) | d; }
 
+// (src, dst) → arc slot: open addressing with linear probing and backward-shift
+// deletion (no tombstones), power-of-two capacity kept under 1/2 load. Keys are
+// never 0 (node ids start at 1), so 0 marks an empty bucket. The incremental
+// stream of a scheduling round (~80k upserts/deletes at config 4) is dominated
+// by these lookups.
+class ArcIndex {
+public:
+    void clear() {
+        keys_.assign(16, 0);
+        vals_.assign(16, -1);
+        size_ = 0;
+    }
+    void reserve(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n + 2) cap <<= 1;
+        if (cap > keys_.size()) rehash(cap);
+    }
+    int find(uint64_t k) const {
+        size_t i = slot(k);
+        while (keys_[i]) {
+            if (keys_[i] == k) return vals_[i];
+            i = (i + 1) & mask();
+        }
+        return -1;
+    }
+    void insert(uint64_t k, int v) {   // k must be absent
+        if (2 * (size_ + 1) > keys_.size()) rehash(keys_.size() * 2);
+        size_t i = slot(k);
+        while (keys_[i]) i = (i + 1) & mask();
+        keys_[i] = k;
+        vals_[i] = v;
+        ++size_;
+    }
+    void erase(uint64_t k) {
+        size_t i = slot(k);
+        while (keys_[i] && keys_[i] != k) i = (i + 1) & mask();
+        if (!keys_[i]) return;
+        // backward shift: pull later members of the probe run into the hole
+        size_t j = i;
+        for (;;) {
+            j = (j + 1) & mask();
+            if (!keys_[j]) break;
+            const size_t h = slot(keys_[j]);
+            const bool between = (i <= j) ? (i < h && h <= j) : (i < h || h <= j);
+            if (between) continue;
+            keys_[i] = keys_[j];
+            vals_[i] = vals_[j];
+            i = j;
+        }
+        keys_[i] = 0;
+        vals_[i] = -1;
+        --size_;
+    }
+
+private:
+    std::vector<uint64_t> keys_ = std::vector<uint64_t>(16, 0);
+    std::vector<int> vals_ = std::vector<int>(16, -1);
+    size_t size_ = 0;
+    size_t mask() const { return keys_.size() - 1; }
+    size_t slot(uint64_t k) const {
+        k ^= k >> 33;
+        k *= 0xff51afd7ed558ccdULL;
+        k ^= k >> 33;
+        return (size_t)k & mask();
+    }
+    void rehash(size_t cap) {
+        std::vector<uint64_t> ok;
+        std::vector<int> ov;
+        ok.swap(keys_);
+        ov.swap(vals_);
+        keys_.assign(cap, 0);
+        vals_.assign(cap, -1);
+        size_ = 0;
+        for (size_t i = 0; i < ok.size(); ++i)
+            if (ok[i]) insert(ok[i], ov[i]);
+    }
+};
+
 }  // namespace
 
 struct ks_ctx {
@@ -54,7 +131,7 @@ struct ks_ctx {
     std::vector<NodeRec> nodes;            // index = NodeID (slot 0 unused)
     std::vector<ArcRec> arcs;
     std::vector<int> free_arcs;
-    std::unordered_map<uint64_t, int> arc_of;
+    ArcIndex arc_of;
     std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy)
     bool dirty = true;
     bool reloaded = true;                  // ks_load_graph since the last solve: no warm start
@@ -104,11 +181,8 @@ int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int6
         return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has low > cap");
     if (cap > (int64_t(1) << 53) || cost > (int64_t(1) << 40) || cost < -(int64_t(1) << 40))
         return c->fail(KS_E_RANGE, "arc capacity or cost outside the supported range");
-    auto it = c->arc_of.find(arc_key(s, d));
-    int slot;
-    if (it != c->arc_of.end()) {
-        slot = it->second;
-    } else {
+    int slot = c->arc_of.find(arc_key(s, d));
+    if (slot < 0) {
         if (!c->free_arcs.empty()) {
             slot = c->free_arcs.back();
             c->free_arcs.pop_back();
@@ -116,7 +190,7 @@ int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int6
             slot = (int)c->arcs.size();
             c->arcs.emplace_back();
         }
-        c->arc_of.emplace(arc_key(s, d), slot);
+        c->arc_of.insert(arc_key(s, d), slot);
         c->arcs[slot].prev_up = -1;
         c->inc[s].push_back(slot);
         c->inc[d].push_back(slot);
@@ -177,25 +251,29 @@ int upload(ks_ctx* c) {
         }
     }
     if (c->opts.auto_sink && nsinks == 1) c->c_supply[sink] = -others;
-    c->up_arc.clear();
-    c->c_src.clear();
-    c->c_dst.clear();
-    c->c_low.clear();
-    c->c_cap.clear();
-    c->c_cost.clear();
-    c->c_prev.clear();
     const bool warm = c->opts.warm_start && !c->reloaded;
+    const size_t live = c->arcs.size() - c->free_arcs.size();
+    c->up_arc.resize(live);
+    c->c_src.resize(live);
+    c->c_dst.resize(live);
+    c->c_low.resize(live);
+    c->c_cap.resize(live);
+    c->c_cost.resize(live);
+    c->c_prev.resize(warm ? live : 0);
+    size_t k = 0;
     for (int slot = 0; slot < (int)c->arcs.size(); ++slot) {
         const ArcRec& a = c->arcs[slot];
         if (!a.alive) continue;
-        c->up_arc.push_back(slot);
-        c->c_src.push_back((int32_t)(a.src - 1));
-        c->c_dst.push_back((int32_t)(a.dst - 1));
-        c->c_low.push_back(a.low);
-        c->c_cap.push_back(a.cap);
-        c->c_cost.push_back(a.cost);
-        if (warm) c->c_prev.push_back(a.prev_up);
+        c->up_arc[k] = slot;
+        c->c_src[k] = (int32_t)(a.src - 1);
+        c->c_dst[k] = (int32_t)(a.dst - 1);
+        c->c_low[k] = a.low;
+        c->c_cap[k] = a.cap;
+        c->c_cost[k] = a.cost;
+        if (warm) c->c_prev[k] = a.prev_up;
+        ++k;
     }
+    if (k != live) return c->fail(KS_E_INVALID, "internal: arc free list out of sync");
     if (warm) {
         c->c_fresh.assign(n, 0);
         for (int64_t v = 0; v < n; ++v) c->c_fresh[v] = c->nodes[v + 1].alive && c->nodes[v + 1].fresh;
@@ -273,7 +351,7 @@ void ks_default_opts(ks_opts* o) {
     o->auto_sink = 1;
     o->price_refine = 1;
     o->gu_interval = 32;
-    o->warm_start = 1;
+    o->warm_start = 0;
 }
 
 ks_ctx* ks_create(int device, const ks_opts* opts) {
@@ -303,14 +381,29 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     c->arcs.clear();
     c->free_arcs.clear();
     c->arc_of.clear();
-    c->arc_of.reserve(m * 2 + 16);
+    c->arc_of.reserve(m);
     c->arcs.reserve(m);
     c->have_solution = false;
     c->dirty = true;
     c->reloaded = true;
+    uint64_t maxid = 0;
+    for (size_t i = 0; i < n; ++i) maxid = std::max<uint64_t>(maxid, nodes[i].id);
+    if (maxid < kMaxId) {
+        c->nodes.reserve(maxid + 1);
+        c->inc.reserve(maxid + 1);
+    }
     for (size_t i = 0; i < n; ++i) {
         int rc = add_node(c, nodes[i].id, nodes[i].excess, nodes[i].type);
         if (rc) return rc;
+    }
+    {   // size the incidence lists once (one pass over the arcs)
+        std::vector<uint32_t> deg(c->nodes.size(), 0);
+        for (size_t i = 0; i < m; ++i) {
+            if (arcs[i].src < deg.size()) ++deg[arcs[i].src];
+            if (arcs[i].dst < deg.size()) ++deg[arcs[i].dst];
+        }
+        for (size_t v = 0; v < deg.size(); ++v)
+            if (deg[v]) c->inc[v].reserve(deg[v]);
     }
     for (size_t i = 0; i < m; ++i) {
         const ks_arc& a = arcs[i];
@@ -346,8 +439,8 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
                 break;
             case KS_UPDATE_ARC: {
                 if (x.low == 0 && x.cap == 0) {  // DeleteArc / ChangeArc(0,0): no capacity left
-                    auto it = c->arc_of.find(arc_key(x.src, x.dst));
-                    if (it != c->arc_of.end()) kill_arc(c, it->second);
+                    const int slot = c->arc_of.find(arc_key(x.src, x.dst));
+                    if (slot >= 0) kill_arc(c, slot);
                     else if (!node_alive(c, x.src) || !node_alive(c, x.dst))
                         rc = c->fail(KS_E_INVALID, "update of arc with a missing endpoint");
                     break;

@@ -35,7 +35,7 @@ def test_abi_version_and_default_opts():
     assert lib.ks_abi_version() == 1
     o = native.default_opts()
     assert (o.alpha, o.verify, o.auto_sink) == (8, 1, 1)
-    assert o.price_refine == 1 and o.gu_interval > 0 and o.warm_start == 1
+    assert o.price_refine == 1 and o.gu_interval > 0 and o.warm_start == 0
 
 
 def test_create_fails_loudly_without_device():

@@ -11,11 +11,14 @@ from oracle import ko
 pytestmark = pytest.mark.gpu
 
 
-def test_incremental_rounds_match_full_resolve(ctx):
+@pytest.mark.parametrize("warm", [0, 1])
+def test_incremental_rounds_match_full_resolve(warm):
     """Config 4 at config-2 scale: pins, completions, arrivals, ageing and
     capacity refresh as one delta stream per round; the device result after
-    applying the deltas equals the oracle on the cell's full graph."""
+    applying the deltas equals the oracle on the cell's full graph, re-solved
+    from scratch (warm_start 0) or from the previous flow and prices (1)."""
     cell = churn.Cell(10_000, 1_000, 25, 100, 2)
+    ctx = native.Context(0, warm_start=warm)
     ctx.load_graph(cell.graph())
     r = ctx.solve()
     mp = ctx.task_mapping()
@@ -27,7 +30,7 @@ def test_incremental_rounds_match_full_resolve(ctx):
         st, cost, flow, _ = ko.cost_scaling(g)
         assert st == 0
         assert (r.cost, r.flow) == (cost, flow), f"round {rnd + 1}"
-        assert r.raw["warm_started"] == 1          # re-solved from the previous flow and prices
+        assert r.raw["warm_started"] == warm
         fl = flows_by_arc(ctx, g)
         vst, vcost, _ = ko.verify(g, fl)
         assert vst == 0 and vcost == cost
@@ -36,6 +39,7 @@ def test_incremental_rounds_match_full_resolve(ctx):
         # every running task stays on its PU (its running arc has low = 1)
         for t in cell.task_ids(cell.RUN).tolist():
             assert mp[t] == int(cell.pu[t - cell.TASK0])
+    ctx.close()
 
 
 def test_solve_many_matches_oracle():
@@ -94,7 +98,7 @@ def test_union_batch_matches_parts(ctx):
 def test_warm_resolve_without_changes_and_cold_opt_out():
     g = gen.quincy(2_000, 200, 8, 20, 77)
     st, cost, flow, _ = ko.cost_scaling(g)
-    with native.Context(0) as c:
+    with native.Context(0, warm_start=1) as c:
         c.load_graph(g)
         r0 = c.solve()
         r1 = c.solve()                           # same graph: warm identity start

@@ -1,9 +1,13 @@
 #!/bin/bash
-# Sweep an env variable over values on config3 (3 repeats each, 5 steps).
+# Interleaved env-variant comparison on the full bench: VARIANTS="X=1;KS_A=2 KS_B=3;..." tools/exp_env.sh out
 set -o pipefail
-OUT=gpurun_out/${1:-env}; VAR=$2; VALS=$3
+OUT=gpurun_out/${1:-envx}
 mkdir -p "$OUT"
-for r in 1 2; do for val in $VALS; do
-  env $VAR=$val timeout -k 10 120 python -u bench.py --steps 5 --warmup 1 --cpu-baseline off ${@:4} > "$OUT/b_${val}_$r.json" 2>"$OUT/b_${val}_$r.err" || { tail -5 "$OUT/b_${val}_$r.err"; exit 1; }
-  python -c "import json; d=json.load(open('$OUT/b_${val}_$r.json')); s=d['solve']; print('$VAR=$val', d['ms_per_step'], 'ph', s['phases'], 'sw', s['sweeps'], 'gus', s['global_updates'], 'bfr', s['gu_iterations'], 'pr_ms', round(s['ms']['global_update'],2))"
-done; done
+IFS=';' read -ra VS <<< "${VARIANTS:-X=1}"
+for rep in 1 2; do
+    for i in "${!VS[@]}"; do
+        e=${VS[$i]}
+        env $e timeout -k 10 120 python -u bench.py --steps 8 --warmup 1 --cpu-baseline off ${ARGS} > "$OUT/v${i}_$rep.json" 2>/dev/null || { echo "fail $e"; exit 1; }
+        python -c "import json; d=json.load(open('$OUT/v${i}_$rep.json')); s=sorted(d['step_ms']); x=d['solve']; print('%-40s mean %7.2f med %7.2f min %7.2f | sw %5d gus %4d bfr %5d bfl %5d' % ('$e', d['ms_per_step'], s[len(s)//2], s[0], x['sweeps'], x['global_updates'], x['gu_iterations'], x['gu_launches']))"
+    done
+done
