@@ -43,5 +43,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def variant_path(tag: str) -> str:
+    return os.path.join(HERE, f"libksmcmf_{tag}.so")
+
+
+def build_variant(tag: str, defines: list[str]) -> str:
+    """An extra copy of the library compiled with -D<defines> (tuning experiments)."""
+    out = variant_path(tag)
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines],
+           *SOURCES, "-o", out + ".tmp"]
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

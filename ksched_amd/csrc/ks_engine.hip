@@ -68,7 +68,10 @@ constexpr int NGC = 6;             // group classes: 4, 8, 16, 32, 64 lanes; 64 
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
 constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
 constexpr int PER_T = CHUNK / 256; // arcs per thread in a hub chunk
-constexpr int WPW = 4;             // windows per wave in sparse (grid-stride) passes
+#ifndef KS_WPW
+#define KS_WPW 2
+#endif
+constexpr int WPW = KS_WPW;        // windows per wave in sparse (grid-stride) passes
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -155,6 +158,7 @@ struct DG {
     unsigned* trace;   // optional per-sweep [visits, relabels, groups, heavy] (KS_TRACE)
     unsigned long long* stamps;   // optional per-block [t0, t1, kind|active] of one sweep (KS_STAMP)
     int stamp_sweep;
+    int chunk_claim;   // 1: chunked nodes use the claim/arrive protocol (KS_CHUNK_CLAIM)
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -807,6 +811,86 @@ __device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, con
     if (lane == 0) settle(g, F, N, slot, x, ci.nch, false, take, Ac, minc, px, PN, eps, out, c);
 }
 
+// Whole-node discharge by one wave (chunked class, 65..4096 arcs): the wave of
+// the node's lead chunk item loads its arcs NB×64 at a time (all loads of a
+// batch issued together, then the price gathers), distributes the excess with
+// one wave scan per 64 arcs and relabels like sweep_group. One dependent chain
+// per batch instead of the claim/arrive protocol of hubs.
+template <int NB>
+__device__ void node_discharge(const DG& g, const Front& F, const Front& N, int x,
+                               const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
+                               Pend& pd, int& out, Cnt& c) {
+    const int lane = lane_id();
+    if (lane == 0) F.flag[x] = 0;   // the lead consumes the node's flag
+    const long long e = atom_load(&g.excess[x]);
+    if (e <= 0) return;
+    const long long px = P[x];
+    const int b0 = g.first[x], en = g.first[x + 1];
+    if (lane == 0) c.visit++;
+    long long rem = e, minc = INF64;
+    for (int base = b0; base < en; base += 64 * NB) {
+        long long r[NB], cs[NB], pw[NB];
+        int w[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int a = base + j * 64 + lane;
+            r[j] = 0;
+            cs[j] = 0;
+            w[j] = 0;
+            if (a < en) {
+                r[j] = g.rcap[a];
+                w[j] = g.head[a];
+                cs[j] = g.cost[a];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) pw[j] = (base + j * 64 + lane < en) ? P[w[j]] : 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int a = base + j * 64 + lane;
+            const bool valid = a < en;
+            const long long cr = cs[j] + px - pw[j];
+            const long long adm = (valid && cr < 0 && r[j] > 0) ? r[j] : 0;
+            long long d = 0;
+            if (rem > 0) {   // wave-uniform
+                const long long incl = wave_incl_scan(adm, lane);
+                const long long total = __shfl(incl, WAVE - 1);
+                d = rem - (incl - adm);
+                d = d < 0 ? 0 : (d > adm ? adm : d);
+                if (d > 0) {
+                    push_arc(g, &N, a, w[j], r[j], d, pd, out);
+                    c.push++;
+                }
+                rem -= total < rem ? total : rem;
+            }
+            if (valid) {
+                c.scan++;
+                if (cr < 0) {
+                    if (r[j] - d > 0) minc = min(minc, cr);
+                } else if (r[j] > 0 || cr <= eps) {
+                    minc = min(minc, cr);
+                }
+            }
+        }
+        flush_pending(g, &N, pd, out);
+        if (rem == 0) break;   // no relabel needed: the rest of the arcs need no scan
+    }
+    minc = wave_min(minc);
+    if (lane == 0) {
+        const long long pushed = e - rem;
+        if (pushed) atom_add(&g.excess[x], -pushed);
+        long long np = px;
+        if (rem > 0) {
+            if (minc >= INF64) g.ctl->infeasible = 1;
+            else np = px - (minc + eps);
+            c.relabel++;
+            N.flag[x] = 1;
+            out = 1;
+        }
+        PN[x] = np;
+    }
+}
+
 // ------------------------------------------------------ grid-stride windows ---
 // Sparse passes use a one-generation grid: each wave owns WPW windows (class
 // windows, then chunk items) strided across the grid, ballots all their flags
@@ -891,7 +975,12 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
-                chunk_discharge(g, F, N, g.citems[w - g.wbeg[CCLS]], P, PN, eps, pd, out, c);
+                const CItem ci = g.citems[w - g.wbeg[CCLS]];
+                if (!g.chunk_claim) {
+                    if (ci.lead) node_discharge<8>(g, F, N, ci.node, P, PN, eps, pd, out, c);
+                } else {
+                    chunk_discharge(g, F, N, ci, P, PN, eps, pd, out, c);
+                }
                 continue;
             }
             switch (class_of_window(g, w)) {
@@ -1902,6 +1991,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     {
         const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
         g.expand = ex ? std::atoi(ex) : 1;
+        const char* cc = std::getenv("KS_CHUNK_CLAIM");
+        g.chunk_claim = cc ? std::atoi(cc) : 0;
     }
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round

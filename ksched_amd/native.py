@@ -66,7 +66,10 @@ _LIB = None
 
 
 def lib_path() -> str:
-    return _build.LIB
+    """The in-tree library; KS_LIB_VARIANT=<tag> selects libksmcmf_<tag>.so built
+    by _build.build_variant (compile-time tuning experiments)."""
+    tag = os.environ.get("KS_LIB_VARIANT")
+    return _build.variant_path(tag) if tag else _build.LIB
 
 
 def load(build_if_missing: bool = True):
