@@ -158,7 +158,6 @@ struct DG {
     unsigned* trace;   // optional per-sweep [visits, relabels, groups, heavy] (KS_TRACE)
     unsigned long long* stamps;   // optional per-block [t0, t1, kind|active] of one sweep (KS_STAMP)
     int stamp_sweep;
-    int chunk_claim;   // 1: chunked nodes use the claim/arrive protocol (KS_CHUNK_CLAIM)
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -659,8 +658,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
 }
 
 // -------------------------------------------------- chunked claim protocol ---
-// Hubs (one workgroup per 1024-arc chunk) and chunked-class nodes (one wave per
-// 64-arc chunk) discharge cooperatively. Every chunk reads the node's excess E
+// Hubs (one workgroup per 1024-arc chunk) discharge cooperatively. Every chunk reads the node's excess E
 // once, requests its admissible capacity Ac with ONE returning atomicAdd on the
 // node's request counter (no CAS loop), takes clamp(E − start, 0, Ac), pushes,
 // and reports (taken, relabel minimum, unsaturated). The last-arriving chunk
@@ -769,47 +767,6 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
 }
 
 // Chunked-class discharge: one wave per 64-arc chunk of node x (flagged in F).
-__device__ void chunk_discharge(const DG& g, const Front& F, const Front& N, const CItem& ci,
-                                const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
-                                Pend& pd, int& out, Cnt& c) {
-    const int lane = lane_id();
-    const int x = ci.node;
-    const long long px = P[x];
-    const long long E = atom_load(&g.excess[x]);
-    const int a = ci.begin + lane;
-    long long r = 0, cr = 0;
-    int w = 0;
-    if (a < ci.end) {
-        r = g.rcap[a];
-        w = g.head[a];
-        cr = g.cost[a] + px - P[w];
-        c.scan++;
-    }
-    const long long adm = (a < ci.end && cr < 0 && r > 0) ? r : 0;
-    const long long incl = wave_incl_scan(adm, lane);
-    const long long Ac = __shfl(incl, WAVE - 1);
-    const int slot = g.nheavy + (x - g.obeg[CCLS]);
-    long long take = 0;
-    if (lane == 0) take = claim(g, slot, E, Ac);
-    take = __shfl(take, 0);
-    long long d = take - (incl - adm);
-    d = d < 0 ? 0 : (d > adm ? adm : d);
-    if (d > 0) {
-        push_arc(g, &N, a, w, r, d, pd, out);
-        c.push++;
-    }
-    long long minc = INF64;
-    if (a < ci.end) {
-        if (cr < 0) {
-            if (r - d > 0) minc = cr;
-        } else if (r > 0 || cr <= eps) {
-            minc = cr;
-        }
-    }
-    flush_pending(g, &N, pd, out);
-    minc = wave_min(minc);
-    if (lane == 0) settle(g, F, N, slot, x, ci.nch, false, take, Ac, minc, px, PN, eps, out, c);
-}
 
 // Whole-node discharge by one wave (chunked class, 65..4096 arcs): the wave of
 // the node's lead chunk item loads its arcs NB×64 at a time (all loads of a
@@ -976,11 +933,7 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
                 const CItem ci = g.citems[w - g.wbeg[CCLS]];
-                if (!g.chunk_claim) {
-                    if (ci.lead) node_discharge<8>(g, F, N, ci.node, P, PN, eps, pd, out, c);
-                } else {
-                    chunk_discharge(g, F, N, ci, P, PN, eps, pd, out, c);
-                }
+                if (ci.lead) node_discharge<8>(g, F, N, ci.node, P, PN, eps, pd, out, c);
                 continue;
             }
             switch (class_of_window(g, w)) {
@@ -1991,8 +1944,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     {
         const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
         g.expand = ex ? std::atoi(ex) : 1;
-        const char* cc = std::getenv("KS_CHUNK_CLAIM");
-        g.chunk_claim = cc ? std::atoi(cc) : 0;
     }
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
@@ -2001,12 +1952,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi_base = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
-    int gi_tail = 0;
-    long long tail_units = 1;
-    if (const char* e = std::getenv("KS_GI_TAIL")) gi_tail = std::max(2, std::min(MAXB, std::atoi(e))) & ~1;
-    if (const char* e = std::getenv("KS_GI_TAIL_UNITS")) tail_units = std::max(1LL, std::atoll(e));
-    int sat_eps = 0;   // KS_SAT_EPS=1: phase start saturates only arcs violating the new ε
-    if (const char* e = std::getenv("KS_SAT_EPS")) sat_eps = std::atoi(e);
     const int pr_cap = 160;                        // price-refinement rounds before giving up
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
@@ -2101,12 +2046,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
         hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g,
-                           phases == 1 && use_warm ? warm_thr : (sat_eps ? eps : 0LL));
+                           phases == 1 && use_warm ? warm_thr : 0LL);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         bool gu_running = false;
         uint64_t phase_sweeps = 0;
-        // sweeps per update: gi, or gi_tail once ε is below tail_units cost units
-        const int gi = (gi_tail > 0 && eps < tail_units * mult) ? gi_tail : gi_base;
+        const int gi = gi_base;
         int gu_r0 = 0;   // bf_count when the running update started
         for (;;) {
             // one cycle: [GU init] [kb BF rounds] [max] [apply] [gi sweeps]
