@@ -43,6 +43,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+DAEMON = os.path.join(HERE, "ks_flow_scheduler")
+DAEMON_SRC = os.path.join(CSRC, "ks_flow_scheduler.cpp")
+
+
+def build_daemon(force: bool = False) -> str:
+    """The flow_scheduler-compatible DIMACS daemon, linked against the in-tree library."""
+    if not force and os.path.exists(DAEMON) and os.path.getmtime(DAEMON) >= max(
+            os.path.getmtime(DAEMON_SRC), os.path.getmtime(LIB)):
+        return DAEMON
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), DAEMON_SRC,
+           "-L" + HERE, "-lksmcmf", "-Wl,-rpath,$ORIGIN", "-o", DAEMON + ".tmp"]
+    subprocess.run(cmd, check=True)
+    os.replace(DAEMON + ".tmp", DAEMON)
+    return DAEMON
+
+
 def variant_path(tag: str) -> str:
     return os.path.join(HERE, f"libksmcmf_{tag}.so")
 
@@ -60,3 +76,4 @@ def build_variant(tag: str, defines: list[str]) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_daemon(force=True))

@@ -130,6 +130,19 @@ def bfs_mapping(g, flow, cost: int = 0):
     return dict(zip(tk[:k].tolist(), pu[:k].tolist()))
 
 
+def bfs_mapping_from_text(g, text: str):
+    """Reference-faithful parseFlowToMapping over an "f"/"s"/"c EOI" text block
+    (e.g. a solver daemon's output); raises like solver.go:223-225."""
+    h = _Holder(g)
+    raw = text.encode()
+    tk = np.zeros(h.ntype.shape[0] + 1, np.int64)
+    pu = np.zeros(h.ntype.shape[0] + 1, np.int64)
+    k = lib().ko_bfs_mapping_from_lines(C.byref(h.kg), raw, len(raw), _p(tk), _p(pu))
+    if k < 0:
+        raise RuntimeError("Task Node to Resource Node should be 1:1 mapping")
+    return dict(zip(tk[:k].tolist(), pu[:k].tolist()))
+
+
 def gen_quincy(T, M, R, J, seed):
     """The C generator's arrays (to check the numpy twin bit-for-bit)."""
     n, m = C.c_int64(), C.c_int64()

@@ -71,6 +71,28 @@ def apply_deltas_to_arcs(nodes: dict, arcs: dict, deltas) -> None:
             nodes[int(x["id"])][0] = int(x["excess"])
 
 
+def dimacs_changes(deltas) -> str:
+    """ks_delta records as the incremental DIMACS text of dimacs/*_change.go
+    (GenerateChange), terminated by "c EOI" (dimacs/export.go:31-38)."""
+    out = []
+    for x in deltas:
+        k = int(x["kind"])
+        if k == 0:
+            out.append(f"n {int(x['id'])} {int(x['excess'])} {int(x['type'])}")
+        elif k == 1:
+            out.append(f"r {int(x['id'])}")
+        elif k == 2:
+            out.append(f"a {int(x['src'])} {int(x['dst'])} {int(x['low'])} {int(x['cap'])} {int(x['cost'])} "
+                       f"{int(x['type'])}")
+        elif k == 3:
+            out.append(f"x {int(x['src'])} {int(x['dst'])} {int(x['low'])} {int(x['cap'])} {int(x['cost'])} "
+                       f"{int(x['type'])} {int(x['old_cost'])}")
+        else:
+            raise ValueError("SET_EXCESS has no DIMACS record")
+    out.append("c EOI")
+    return "\n".join(out) + "\n"
+
+
 def graph_from_store(nodes: dict, arcs: dict):
     n = max(nodes) if nodes else 0
     ntype = np.zeros(n, np.int32)
