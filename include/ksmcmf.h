@@ -180,13 +180,18 @@ int ks_solve_many(ks_ctx* const* ctxs, size_t k, int workers, ks_result* results
 /* Arcs with positive flow from the last solve (the "f" lines). */
 int ks_get_flows(ks_ctx* ctx, ks_flow* out, size_t cap, size_t* count);
 
-/* task NodeID → PU NodeID for every task whose unit reaches a PU (TaskMapping). */
+/* task NodeID → PU NodeID for every task whose unit reaches a PU (TaskMapping).
+ * The flow is decomposed on the device: each task's unit is followed along
+ * positive-flow arcs (units numbered per node in arc order) to the sink, and
+ * the last PU on the way is its placement. */
 int ks_get_task_mapping(ks_ctx* ctx, uint64_t* task, uint64_t* pu,
                         size_t cap, size_t* count);
 
 /* Device-resident mapping for RCCL gathers: for the i-th task node in id order
- * writes the PU node id it maps to, or 0 when unscheduled. dev_out is a device
- * pointer with room for `cap` uint64; *count receives the number of task nodes. */
+ * writes the PU node id it maps to, or 0 when unscheduled, computed on device
+ * (nothing crosses PCIe). dev_out is a device pointer with room for `cap`
+ * uint64 (KS_E_INVALID when cap < the task count); dev_out = NULL only sets
+ * *count, the number of task nodes. */
 int ks_get_task_pu_device(ks_ctx* ctx, uint64_t* dev_out, size_t cap, size_t* count);
 
 #ifdef __cplusplus

@@ -33,8 +33,8 @@ public:
     // be null (no warm start for this graph).
     int upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
                const int64_t* low, const int64_t* cap, const int64_t* cost,
-               const int64_t* supply, const int32_t* prev_idx, const uint8_t* fresh,
-               std::string& err);
+               const int64_t* supply, const uint8_t* type, const int32_t* prev_idx,
+               const uint8_t* fresh, std::string& err);
 
     // Build the residual CSR on device and run ε-scaling push-relabel to
     // optimality, then verify on device. Fills r (never NULL here).
@@ -43,6 +43,16 @@ public:
 
     // Flow on every input arc (input order) from the last successful solve.
     int download_flows(int64_t* flows, std::string& err);
+
+    // Task → PU placement of the last solve, decomposed on device: for the i-th
+    // task slot (DIMACS type 1) in slot order, the node id (slot + 1) of the last
+    // PU its flow unit crosses, 0 when unscheduled. *count = number of tasks;
+    // dev_out (device memory, ≥ count entries) may be null to query the count.
+    int task_pu(uint64_t* dev_out, size_t cap, size_t* count, std::string& err);
+
+    // Engine-owned device scratch of n uint64 (valid until the next call).
+    int scratch(uint64_t** dev, size_t n, std::string& err);
+    int download(void* host_dst, const void* dev_src, size_t bytes, std::string& err);
 
     // Copy host bytes to a caller-provided device pointer on the engine stream.
     int copy_to_device(void* dev_dst, const void* host_src, size_t bytes, std::string& err);

@@ -1455,6 +1455,75 @@ __global__ void k_save_prices(int n, const int* __restrict__ perm, const long lo
         pslot[v] = p0[perm[v]];
 }
 
+// ================================================ task → PU mapping ===
+// Path decomposition of the solved flow on device (replaces parseFlowToMapping,
+// placement/solver.go:183-269). Flow units are numbered per node: the units
+// leaving x are numbered along x's forward arcs in CSR order (out prefix), the
+// units entering y along y's reverse arcs (in prefix); unit k entering y leaves
+// on y's k-th outgoing unit. A task's single unit is followed until it reaches a
+// node without outflow (the sink); the last PU on the way is its placement.
+__global__ void k_unit_vals(long long m2, const int* __restrict__ vals, const long long* __restrict__ flows,
+                            long long* __restrict__ outv, long long* __restrict__ inv) {
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
+        const int v = vals[p];
+        const long long f = flows[v >> 1];
+        outv[p] = (v & 1) ? 0 : f;
+        inv[p] = (v & 1) ? f : 0;
+    }
+}
+
+__global__ void k_node_meta(int n, const int* __restrict__ perm, const unsigned char* __restrict__ type,
+                            int* __restrict__ iperm, unsigned char* __restrict__ itype, int* __restrict__ is_task) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+        const int x = perm[v];
+        iperm[x] = (int)v;
+        itype[x] = type[v];
+        is_task[v] = type[v] == KS_NODE_TASK ? 1 : 0;
+    }
+}
+
+// smallest position p in [lo, hi) with pre[p] + val[p] > k (pre is the inclusive-
+// exclusive pair of a scan: pre[p] = units before p within the segment)
+__device__ __forceinline__ int find_unit(const long long* __restrict__ scan, const long long* __restrict__ val,
+                                         int lo, int hi, long long base, long long k) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (scan[mid] - base + val[mid] <= k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_task_paths(int n, int nn, const int* __restrict__ perm, const int* __restrict__ first,
+                             const int* __restrict__ head, const int* __restrict__ rev,
+                             const long long* __restrict__ outv, const long long* __restrict__ outs,
+                             const long long* __restrict__ inv, const long long* __restrict__ ins,
+                             const int* __restrict__ iperm, const unsigned char* __restrict__ itype,
+                             const int* __restrict__ rank, const unsigned char* __restrict__ type,
+                             unsigned long long* __restrict__ out) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+        if (type[v] != KS_NODE_TASK) continue;
+        int x = perm[v];
+        long long k = 0;   // unit index among x's outgoing units
+        int last_pu = -1;
+        for (int step = 0; step <= nn; ++step) {
+            const int lo = first[x], hi = first[x + 1];
+            if (lo >= hi) break;
+            const long long obase = outs[lo];
+            const long long otot = outs[hi - 1] + outv[hi - 1] - obase;
+            if (k >= otot) break;   // absorbed here (no outflow left)
+            const int p = find_unit(outs, outv, lo, hi, obase, k);
+            const long long off = k - (outs[p] - obase);
+            const int y = head[p];
+            if (itype[y] == KS_NODE_PU) last_pu = y;
+            const int q = rev[p];
+            k = ins[q] - ins[first[y]] + off;
+            x = y;
+        }
+        out[rank[v]] = last_pu >= 0 ? (unsigned long long)iperm[last_pu] + 1 : 0ULL;
+    }
+}
+
 // ============================================================ host helpers ===
 inline int grid_for(long long n, int cap = 4096) {
     long long b = (n + BLK - 1) / BLK;
@@ -1497,6 +1566,7 @@ struct EngineImpl {
     int64_t maxc = 0;
     DBuf<int> a_src, a_dst;
     DBuf<long long> a_low, a_cap, a_cost, supply;
+    DBuf<unsigned char> a_type;   // DIMACS node type per slot (task/PU for the mapping)
 
     // residual CSR and node state, internal ids
     DBuf<unsigned> keys_in, keys_out;
@@ -1533,6 +1603,12 @@ struct EngineImpl {
     int map_state = 0;             // 0 no mapping, 1 same arcs as the last solve, 2 a_prev
     int64_t n_prev = 0;
     long long mult_prev = 1;
+    // device mapping extraction scratch
+    DBuf<long long> map_outv, map_inv, map_outs, map_ins;
+    DBuf<int> map_iperm, map_rank;
+    DBuf<unsigned char> map_itype, map_tmp;
+    DBuf<uint64_t> map_scratch;   // device vector behind ks_get_task_mapping
+    int64_t n_tasks = 0;
 
     ~EngineImpl() {
         if (stream) {
@@ -1549,6 +1625,8 @@ struct EngineImpl {
         q_arrive.release(); q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
         ctr.release(); trace.release(); stamps.release(); ctl.release();
         a_prev.release(); a_fresh.release(); prev_flows.release(); p_slot.release();
+        a_type.release(); map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release();
+        map_iperm.release(); map_itype.release(); map_rank.release(); map_tmp.release(); map_scratch.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
         for (auto& e : ev)
@@ -1644,8 +1722,8 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
 }
 
 int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int64_t* low,
-                   const int64_t* cap, const int64_t* cost, const int64_t* supply, const int32_t* prev_idx,
-                   const uint8_t* fresh, std::string& err) {
+                   const int64_t* cap, const int64_t* cost, const int64_t* supply, const uint8_t* type,
+                   const int32_t* prev_idx, const uint8_t* fresh, std::string& err) {
     EngineImpl& s = *p_;
     KS_CHECK(hipSetDevice(s.device));
     if (n < 0 || m < 0 || n > (1LL << 28) || m > (1LL << 29)) {
@@ -1671,6 +1749,10 @@ int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
         KS_CHECK(hipMemcpyAsync(s.a_cost.p, cost, m * sizeof(long long), hipMemcpyHostToDevice, s.stream));
     }
     if (n) KS_CHECK(hipMemcpyAsync(s.supply.p, supply, n * sizeof(long long), hipMemcpyHostToDevice, s.stream));
+    KS_CHECK(s.a_type.ensure(n));
+    s.n_tasks = 0;
+    for (int64_t v = 0; v < n; ++v) s.n_tasks += type[v] == KS_NODE_TASK;
+    if (n) KS_CHECK(hipMemcpyAsync(s.a_type.p, type, n, hipMemcpyHostToDevice, s.stream));
     s.map_state = 0;
     s.fresh_valid = false;
     if (prev_idx && s.has_prev) {
@@ -1684,6 +1766,78 @@ int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
         }
     }
     KS_CHECK(hipStreamSynchronize(s.stream));
+    return KS_OK;
+}
+
+int Engine::task_pu(uint64_t* dev_out, size_t cap, size_t* count, std::string& err) {
+    EngineImpl& s = *p_;
+    if (!s.solved) {
+        err = "no successful solve";
+        return KS_E_INVALID;
+    }
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    *count = (size_t)s.n_tasks;
+    if (!dev_out || cap < (size_t)s.n_tasks || s.n_tasks == 0) {
+        if (dev_out && cap < (size_t)s.n_tasks) {
+            err = "output buffer smaller than the task count";
+            return KS_E_INVALID;
+        }
+        return KS_OK;
+    }
+    const int64_t n = s.n, m2 = 2 * s.m;
+    const int nn = s.nn;
+    KS_CHECK(s.map_outv.ensure(m2));
+    KS_CHECK(s.map_inv.ensure(m2));
+    KS_CHECK(s.map_outs.ensure(m2));
+    KS_CHECK(s.map_ins.ensure(m2));
+    KS_CHECK(s.map_iperm.ensure(nn));
+    KS_CHECK(s.map_itype.ensure(nn));
+    KS_CHECK(s.map_rank.ensure(2 * n));
+    KS_CHECK(hipMemsetAsync(s.map_itype.p, 0, nn, st));
+    if (m2)
+        hipLaunchKernelGGL(k_unit_vals, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, (const int*)s.vals_out.p,
+                           (const long long*)s.flows.p, s.map_outv.p, s.map_inv.p);
+    hipLaunchKernelGGL(k_node_meta, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const int*)s.perm.p,
+                       (const unsigned char*)s.a_type.p, s.map_iperm.p, s.map_itype.p, s.map_rank.p + n);
+    size_t t1 = 0, t2 = 0;
+    if (m2) KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.map_outv.p, s.map_outs.p, (int)m2, st));
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, s.map_rank.p + n, s.map_rank.p, (int)n, st));
+    KS_CHECK(s.map_tmp.ensure(std::max(t1, t2)));
+    size_t tt = s.map_tmp.n;
+    if (m2) {
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_outv.p, s.map_outs.p, (int)m2, st));
+        tt = s.map_tmp.n;
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_inv.p, s.map_ins.p, (int)m2, st));
+    }
+    tt = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_rank.p + n, s.map_rank.p, (int)n, st));
+    hipLaunchKernelGGL(k_task_paths, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, nn, (const int*)s.perm.p,
+                       (const int*)s.first.p, (const int*)s.head.p, (const int*)s.rev.p,
+                       (const long long*)s.map_outv.p, (const long long*)s.map_outs.p,
+                       (const long long*)s.map_inv.p, (const long long*)s.map_ins.p,
+                       (const int*)s.map_iperm.p, (const unsigned char*)s.map_itype.p, (const int*)s.map_rank.p,
+                       (const unsigned char*)s.a_type.p, (unsigned long long*)dev_out);
+    KS_CHECK(hipGetLastError());
+    KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+int Engine::download(void* host_dst, const void* dev_src, size_t bytes, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    if (bytes) {
+        KS_CHECK(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, s.stream));
+        KS_CHECK(hipStreamSynchronize(s.stream));
+    }
+    return KS_OK;
+}
+
+int Engine::scratch(uint64_t** dev, size_t n, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    KS_CHECK(s.map_scratch.ensure(std::max<size_t>(1, n)));
+    *dev = s.map_scratch.p;
     return KS_OK;
 }
 

@@ -141,7 +141,7 @@ struct ks_ctx {
     std::vector<int32_t> c_src, c_dst;
     std::vector<int64_t> c_low, c_cap, c_cost, c_supply;
     std::vector<int32_t> c_prev;
-    std::vector<uint8_t> c_fresh;
+    std::vector<uint8_t> c_fresh, c_type;
     std::vector<int64_t> flows;
     bool have_solution = false;
     bool flows_fresh = false;
@@ -237,12 +237,14 @@ int upload(ks_ctx* c) {
     const int64_t n = (int64_t)maxid;
     c->n_slots = n;
     c->c_supply.assign(n, 0);
+    c->c_type.assign(n, 0);
     int64_t others = 0;
     int64_t sink = -1, nsinks = 0;
     for (int64_t v = 0; v < n; ++v) {
         const NodeRec& r = c->nodes[v + 1];
         if (!r.alive) continue;
         c->c_supply[v] = r.excess;
+        c->c_type[v] = (uint8_t)std::min<int32_t>(std::max<int32_t>(r.type, 0), 255);
         if (r.type == KS_NODE_SINK) {
             sink = v;
             ++nsinks;
@@ -280,7 +282,7 @@ int upload(ks_ctx* c) {
     }
     const int64_t m = (int64_t)c->up_arc.size();
     int rc = c->eng.upload(n, m, c->c_src.data(), c->c_dst.data(), c->c_low.data(), c->c_cap.data(),
-                           c->c_cost.data(), c->c_supply.data(), warm ? c->c_prev.data() : nullptr,
+                           c->c_cost.data(), c->c_supply.data(), c->c_type.data(), warm ? c->c_prev.data() : nullptr,
                            warm ? c->c_fresh.data() : nullptr, c->err);
     if (rc == KS_OK) c->dirty = false;
     return rc;
@@ -293,48 +295,6 @@ int fetch_flows(ks_ctx* c) {
     int rc = c->eng.download_flows(c->flows.data(), c->err);
     if (rc == KS_OK) c->flows_fresh = true;
     return rc;
-}
-
-// Path decomposition of the flow: follow each task's unit along positive-flow
-// arcs (the scheduling network is a DAG) and record the last PU it crosses.
-// Equivalent to parseFlowToMapping (solver.go:183-269) up to the choice among
-// equal-flow decompositions, and correct for mixed-depth DAGs.
-void task_mapping(ks_ctx* c, std::vector<uint64_t>& task, std::vector<uint64_t>& pu) {
-    const int64_t n = c->n_slots, m = (int64_t)c->up_arc.size();
-    std::vector<int> ofirst(n + 2, 0);
-    for (int64_t i = 0; i < m; ++i)
-        if (c->flows[i] > 0) ofirst[c->c_src[i] + 1]++;
-    for (int64_t v = 0; v < n; ++v) ofirst[v + 1] += ofirst[v];
-    std::vector<int> pos(ofirst.begin(), ofirst.end());
-    std::vector<int> odst(ofirst[n] + 1);
-    std::vector<int64_t> orem(ofirst[n] + 1);
-    for (int64_t i = 0; i < m; ++i)
-        if (c->flows[i] > 0) {
-            const int k = pos[c->c_src[i]]++;
-            odst[k] = c->c_dst[i];
-            orem[k] = c->flows[i];
-        }
-    std::vector<int> cur(ofirst.begin(), ofirst.end());
-    task.clear();
-    pu.clear();
-    for (int64_t t = 0; t < n; ++t) {
-        const NodeRec& r = c->nodes[t + 1];
-        if (!r.alive || r.type != KS_NODE_TASK) continue;
-        int64_t v = t, last_pu = -1;
-        for (int64_t steps = 0; steps <= n; ++steps) {
-            if (c->nodes[v + 1].type == KS_NODE_PU) last_pu = v;
-            int k = cur[v];
-            while (k < ofirst[v + 1] && orem[k] == 0) ++k;
-            cur[v] = k;
-            if (k >= ofirst[v + 1]) break;
-            --orem[k];
-            v = odst[k];
-        }
-        if (last_pu >= 0) {
-            task.push_back((uint64_t)t + 1);
-            pu.push_back((uint64_t)last_pu + 1);
-        }
-    }
 }
 
 }  // namespace
@@ -526,42 +486,40 @@ int ks_get_flows(ks_ctx* c, ks_flow* out, size_t cap, size_t* count) {
     return KS_OK;
 }
 
+// Pairs from the device decomposition (Engine::task_pu): the i-th task slot in
+// slot order ↔ the i-th entry of the device vector.
 int ks_get_task_mapping(ks_ctx* c, uint64_t* task, uint64_t* pu, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
-    int rc = fetch_flows(c);
+    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
+    size_t nt = 0;
+    int rc = c->eng.task_pu(nullptr, 0, &nt, c->err);
     if (rc) return rc;
-    std::vector<uint64_t> t, p;
-    task_mapping(c, t, p);
-    *count = t.size();
-    if (task && pu) {
-        const size_t k = std::min(cap, t.size());
-        std::copy(t.begin(), t.begin() + k, task);
-        std::copy(p.begin(), p.begin() + k, pu);
+    uint64_t* dev = nullptr;
+    rc = c->eng.scratch(&dev, nt, c->err);
+    if (rc == KS_OK) rc = c->eng.task_pu(dev, nt, &nt, c->err);
+    std::vector<uint64_t> dense(nt);
+    if (rc == KS_OK) rc = c->eng.download(dense.data(), dev, nt * sizeof(uint64_t), c->err);
+    if (rc) return rc;
+    size_t k = 0, ti = 0;
+    for (int64_t v = 0; v < c->n_slots && ti < nt; ++v) {
+        const NodeRec& r = c->nodes[v + 1];
+        if (!r.alive || r.type != KS_NODE_TASK) continue;
+        const uint64_t p = dense[ti++];
+        if (!p) continue;
+        if (task && pu && k < cap) {
+            task[k] = (uint64_t)v + 1;
+            pu[k] = p;
+        }
+        ++k;
     }
+    *count = k;
     return KS_OK;
 }
 
 int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
-    int rc = fetch_flows(c);
-    if (rc) return rc;
-    std::vector<uint64_t> t, p;
-    task_mapping(c, t, p);
-    std::vector<uint64_t> dense;
-    size_t ti = 0;
-    for (int64_t v = 0; v < c->n_slots; ++v) {
-        const NodeRec& r = c->nodes[v + 1];
-        if (!r.alive || r.type != KS_NODE_TASK) continue;
-        uint64_t val = 0;
-        if (ti < t.size() && t[ti] == (uint64_t)v + 1) val = p[ti++];
-        dense.push_back(val);
-    }
-    *count = dense.size();
-    if (dev_out && cap) {
-        const size_t k = std::min(cap, dense.size());
-        return c->eng.copy_to_device(dev_out, dense.data(), k * sizeof(uint64_t), c->err);
-    }
-    return KS_OK;
+    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
+    return c->eng.task_pu(dev_out, cap, count, c->err);
 }
 
 }  // extern "C"

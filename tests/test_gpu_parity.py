@@ -201,3 +201,24 @@ def test_deltas_match_full_reload(ctx):
     assert st == 0
     assert (r1.cost, r1.flow) == (c, fv)
     assert r0.flow == 1000 and r1.flow == 980
+
+
+def test_device_decomposition_matches_pu_flows(ctx):
+    """The device path decomposition hands out exactly the units each PU sends
+    to the sink: per PU, mapped tasks == flow on PU→sink (every unit through a
+    PU comes from a task in the Quincy shape)."""
+    g = gen.quincy(5000, 500, 20, 50, 31)
+    ctx.load_graph(g)
+    ctx.solve()
+    fl = flows_by_arc(ctx, g)
+    mp = ctx.task_mapping()
+    per_pu = {}
+    for p in mp.values():
+        per_pu[p] = per_pu.get(p, 0) + 1
+    for i in range(g.m):
+        s, d = int(g.src[i]), int(g.dst[i])
+        if g.ntype[s - 1] == 2 and g.ntype[d - 1] == 3:
+            assert per_pu.get(s, 0) == int(fl[i])
+    # and the tasks left unmapped are exactly those whose unit ends unscheduled (→ U_j → sink)
+    sched = sum(int(fl[i]) for i in range(g.m) if g.ntype[int(g.src[i]) - 1] == 2)
+    assert len(mp) == sched
