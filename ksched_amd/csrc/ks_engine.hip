@@ -277,10 +277,16 @@ __device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
 // discharge writes the pair this sweep), the excess a fire-and-forget atomic.
 // Non-hub heads are marked in nf (when given); hub pushes are buffered in pd
 // and flagged once per wave in flush_pending.
+// rv / uc: the arc's reverse position and pair capacity when the caller loaded
+// them with the arc (rv < 0: load them here, one more dependent step).
 __device__ __forceinline__ void push_arc(const DG& g, const Front* nf, int a, int w, long long r, long long d,
-                                         Pend& pd, int& out) {
+                                         Pend& pd, int& out, int rv = -1, long long uc = 0) {
+    if (rv < 0) {
+        rv = g.rev[a];
+        uc = g.ucap[a];
+    }
     g.rcap[a] = r - d;
-    g.rcap[g.rev[a]] = g.ucap[a] - (r - d);
+    g.rcap[rv] = uc - (r - d);
     if (w < g.hub_base) {
         atom_add(&g.excess[w], d);
         if (nf) {
@@ -615,9 +621,13 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         const bool valid = a < en;
         long long r = 0, cr = 0;
         int w = 0;
+        int rv = 0;
+        long long uc = 0;
         if (valid) {
             r = g.rcap[a];
             w = g.head[a];
+            rv = g.rev[a];     // issued with the arc: a push needs no further load
+            uc = g.ucap[a];
             cr = g.cost[a] + pv - P[w];
             c.scan++;
         }
@@ -627,7 +637,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         long long d = rem - (incl - adm);
         d = d < 0 ? 0 : (d > adm ? adm : d);
         if (d > 0) {
-            push_arc(g, &nf, a, w, r, d, pd, out);
+            push_arc(g, &nf, a, w, r, d, pd, out, rv, uc);
             c.push++;
         }
         if (valid) {
@@ -711,17 +721,21 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
     const int x = it.node;
     const long long px = P[x];
     const long long E = atom_load(&g.excess[x]);
-    long long r[PER_T], cr[PER_T], adm[PER_T];
-    int w[PER_T];
+    long long r[PER_T], cr[PER_T], adm[PER_T], uc[PER_T];
+    int w[PER_T], rv[PER_T];
     long long mine = 0;
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
         const int a = it.begin + threadIdx.x * PER_T + k;
         r[k] = 0;
         w[k] = 0;
+        rv[k] = 0;
+        uc[k] = 0;
         if (a < it.end) {
             r[k] = g.rcap[a];
             w[k] = g.head[a];
+            rv[k] = g.rev[a];
+            uc[k] = g.ucap[a];
         }
     }
 #pragma unroll
@@ -749,7 +763,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
         const long long d = adm[k] < rt ? adm[k] : rt;
         rt -= d;
         if (d > 0) {
-            push_arc(g, &N, a, w[k], r[k], d, pd, out);
+            push_arc(g, &N, a, w[k], r[k], d, pd, out, rv[k], uc[k]);
             c.push++;
         }
         if (a < it.end) {
