@@ -73,18 +73,27 @@ def roofline_of(results):
 
 
 class Dist:
-    """torch.distributed over RCCL when launched with WORLD_SIZE > 1."""
+    """torch.distributed over RCCL when launched with WORLD_SIZE > 1.
+
+    KS_BENCH_REHEARSAL=1 (tests only): gloo collectives on host copies and every
+    rank on GPU 0, so the N > 1 code path runs on a one-GPU box."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.rehearsal = os.environ.get("KS_BENCH_REHEARSAL") == "1"
         self.dist = self.torch = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if self.rehearsal:
+                self.local = 0
+                torch.cuda.set_device(0)
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             self.dist, self.torch = dist, torch
 
     def sync(self):
@@ -95,9 +104,15 @@ class Dist:
     def max(self, x: float) -> float:
         if not self.dist:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cpu" if self.rehearsal else "cuda")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def gather(self, block, num_graphs: int):
+        """RCCL all-gather of a device block (rehearsal: gloo on a host copy)."""
+        if self.rehearsal:
+            return batch.gather(block.cpu(), num_graphs, self.dist)
+        return batch.gather(block, num_graphs, self.dist)
 
     def close(self):
         if self.dist:
@@ -154,7 +169,7 @@ def run_full(args, D):
         buf = torch.zeros(1, T, dtype=torch.int64, device="cuda")
         tg0 = time.perf_counter()
         ctx.task_pu_device(buf.data_ptr(), T)
-        out = batch.gather(buf, D.world, D.dist)
+        out = D.gather(buf, D.world)
         torch.cuda.synchronize()
         gather = {"ms": 1e3 * (time.perf_counter() - tg0), "bytes_per_rank": T * 8,
                   "scheduled": int((out > 0).sum().item())}
@@ -299,7 +314,7 @@ def run_batch(args, D):
         else:
             for i, c in enumerate(ctxs):
                 c.task_pu_device(buf[i].data_ptr(), T)
-        full = batch.gather(buf, num, D.dist) if D.dist else buf[:num]
+        full = D.gather(buf, num) if D.dist else buf[:num]
         torch.cuda.synchronize()
         gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
                   "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
