@@ -26,3 +26,8 @@ python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffi
 timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 > "$OUT/bench.json" 2> "$OUT/bench.err" \
     || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
+for wl in incremental batch; do
+    timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --warmup 2 > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" \
+        || { echo "bench $wl failed"; tail -30 "$OUT/bench_$wl.err"; exit 1; }
+    python -c "import json; d=json.load(open('$OUT/bench_$wl.json')); print('$wl', d['ms_per_step'], d['value'], (d.get('cpu_baseline') or {}).get('value'), d.get('parity'))"
+done
