@@ -54,8 +54,6 @@ public:
     int scratch(uint64_t** dev, size_t n, std::string& err);
     int download(void* host_dst, const void* dev_src, size_t bytes, std::string& err);
 
-    // Copy host bytes to a caller-provided device pointer on the engine stream.
-    int copy_to_device(void* dev_dst, const void* host_src, size_t bytes, std::string& err);
 
     int device() const;
 

@@ -108,7 +108,6 @@ constexpr int CCLS = 5;            // chunked class: Bellman-Ford splits its nod
 
 struct CItem {                     // one 64-arc chunk of a chunked-class node
     int node, begin, end, lead;    // lead = 1 for the node's first chunk
-    int nch;                       // chunks of the node
 };
 // A wave owns one window: win_batches(c) batches of 64/G consecutive node ids.
 __host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
@@ -1855,15 +1854,6 @@ int Engine::scratch(uint64_t** dev, size_t n, std::string& err) {
     return KS_OK;
 }
 
-int Engine::copy_to_device(void* dev_dst, const void* host_src, size_t bytes, std::string& err) {
-    EngineImpl& s = *p_;
-    KS_CHECK(hipSetDevice(s.device));
-    if (bytes) {
-        KS_CHECK(hipMemcpyAsync(dev_dst, host_src, bytes, hipMemcpyHostToDevice, s.stream));
-        KS_CHECK(hipStreamSynchronize(s.stream));
-    }
-    return KS_OK;
-}
 
 // "index:path" → index, path
 static bool g_trace_ok(const char* spec, int& idx, std::string& path) {
@@ -2074,16 +2064,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
         std::vector<CItem> ci;
         for (int k = 0; k < cn; ++k) {
-            const int nch = (cf[k + 1] - cf[k] + 63) / 64;
             for (int b = cf[k]; b < cf[k + 1]; b += 64)
-                ci.push_back(CItem{c0 + k, b, std::min(b + 64, cf[k + 1]), b == cf[k] ? 1 : 0, nch});
+                ci.push_back(CItem{c0 + k, b, std::min(b + 64, cf[k + 1]), b == cf[k] ? 1 : 0});
         }
         s.ncitems = (int)ci.size();
         KS_CHECK(s.citems.ensure(std::max<size_t>(1, ci.size())));
         if (!ci.empty())
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
-        // claim slots: hubs, then chunked nodes
-        const int nq = std::max(1, s.nheavy + cn);
+        // claim slots: one per hub
+        const int nq = std::max(1, s.nheavy);
         KS_CHECK(s.q_req.ensure(nq));
         KS_CHECK(s.q_taken.ensure(nq));
         KS_CHECK(s.q_min.ensure(nq));
