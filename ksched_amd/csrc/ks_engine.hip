@@ -1024,14 +1024,29 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 template <bool PR>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
                                             long long eps, long long* hub_min, int& out) {
+    // residual tests of all (≤ 8) arcs issued together; usually one in-arc carries
+    // flow (a task's assignment), so the dependent loads follow for it alone
     const int b0 = g.first[u], b1 = g.first[u + 1];
-    for (int b = b0; b < b1; ++b) {
-        const long long rin = g.ucap[b] - g.rcap[b];
+    unsigned live = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (b0 + k < b1 && g.ucap[b0 + k] - g.rcap[b0 + k] > 0) live |= 1u << k;
+    for (int b = b1 - b0 > 8 ? b0 + 8 : b1; b < b1; ++b)   // leaves have ≤ 8 arcs; kept for safety
+        if (g.ucap[b] - g.rcap[b] > 0) {
+            const int u2 = g.head[b];
+            const long long cand = du + arc_len<PR>(g.p0[u2], g.cost[b], pu, eps);
+            if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[u2] : INF64, hub_min, out)) {
+                nf.flag[u2] = 1;
+                out = 1;
+            }
+        }
+    while (live) {
+        const int b = b0 + __builtin_ctz(live);
+        live &= live - 1;
         const int u2 = g.head[b];
         const long long cb = g.cost[b];
         const long long pu2 = g.p0[u2];
         const long long du2 = u2 < g.hub_base ? g.dist[u2] : INF64;
-        if (rin <= 0) continue;
         const long long cand = du + arc_len<PR>(pu2, cb, pu, eps);
         if (offer<PR>(g, nf, u2, cand, du2, hub_min, out)) {
             nf.flag[u2] = 1;
