@@ -691,13 +691,20 @@ __device__ __forceinline__ void settle(const DG& g, const Front& F, const Front&
     drain_vm();
     const int old = __hip_atomic_fetch_add(&g.q_arrive[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old != nch - 1) return;
+    // every returning atomic of the settle issued together (one round trip), then
+    // one fetch-add applies the taken units and the drained inbox
     const long long mn = atom_exch(&g.q_min[slot], INF64);
     const int unsat = atom_exch_i(&g.q_unsat[slot], 0);
     const long long taken = atom_exch(&g.q_taken[slot], 0);
     atom_exch(&g.q_req[slot], 0LL);
-    if (taken) atom_add(&g.excess[x], -taken);
-    if (hub) drain_inbox(g, x - g.hub_base);
-    const long long now = atom_load(&g.excess[x]);
+    long long inflow = 0;
+    if (hub) {
+        long long* ib = &g.inbox[(x - g.hub_base) * SHARDS];
+#pragma unroll
+        for (int k = 0; k < SHARDS; ++k) inflow += atom_exch(&ib[k], 0LL);
+    }
+    const long long delta = inflow - taken;
+    const long long now = (delta ? atom_add_ret(&g.excess[x], delta) : atom_load(&g.excess[x])) + delta;
     long long np = px;
     if (!unsat && now > 0) {
         if (mn >= INF64) atomicOr(&g.ctl->infeasible, hub ? 2 : 4);
