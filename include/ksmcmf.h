@@ -12,6 +12,9 @@
  *   ks_apply_deltas          placement/solver.go:118-123 writeIncremental →
  *                            dimacs/export.go:31-38 + the GenerateChange methods of
  *                            dimacs/{add_node,create_arc,update_arc,remove_node}_change.go
+ *   ks_coalesce_deltas       the change optimisers graph_change_manager.go:220-279
+ *                            (optimizeChanges: RemoveDuplicate, MergeToSameArc,
+ *                            PurgeBeforeNodeRemoval — declared there, never implemented)
  *   ks_solve                 the external Flowlessly solve (solver.go:30-34, Dockerfile:10-12)
  *                            — min-cost flow, bit-exact total cost and flow value
  *   ks_get_flows             the "f src dst flow" lines read by readFlowGraph
@@ -164,6 +167,17 @@ int ks_load_graph(ks_ctx* ctx, const ks_node* nodes, size_t n,
 
 /* Apply a delta stream in mutation order (later Solves: solver.go:86-88). */
 int ks_apply_deltas(ks_ctx* ctx, const ks_delta* deltas, size_t k);
+
+/* Shrink a delta stream without changing what ks_apply_deltas makes of it
+ * (graph_change_manager.go:220-279): per arc only its last ADD/UPDATE record
+ * survives (both are upserts; UPDATE 0/0 deletes); arc and SET_EXCESS records
+ * touching a node before its REMOVE_NODE are dropped; per node only the last
+ * SET_EXCESS survives. ADD_NODE / REMOVE_NODE records are kept; survivors keep
+ * their order. Host-only (no context, no device). Writes at most `cap` records
+ * to `out` (out == in allowed), *count = surviving records. KS_E_INVALID on a
+ * zero or out-of-range node id. Validation errors a dropped record would have
+ * raised in ks_apply_deltas are not reported. */
+int ks_coalesce_deltas(const ks_delta* in, size_t k, ks_delta* out, size_t cap, size_t* count);
 
 /* Solve min-cost flow on the current graph. result may be NULL. */
 int ks_solve(ks_ctx* ctx, ks_result* result);

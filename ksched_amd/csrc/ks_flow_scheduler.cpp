@@ -17,7 +17,9 @@
 //
 // --daemon=false solves the first graph only. --device=N picks the HIP device.
 // --parse-only parses the stream and prints per-iteration counts without a
-// device (used by the CPU tests). Errors go to stderr with a non-zero exit, the
+// device (used by the CPU tests). --coalesce runs each change block through
+// ks_coalesce_deltas before applying it (the reference's optimizeChanges switches,
+// graph_change_manager.go:220-229; off by default there too). Errors go to stderr with a non-zero exit, the
 // way the reference panics when the pipe breaks.
 #include <cerrno>
 #include <cstdint>
@@ -173,12 +175,13 @@ void emit(ks_ctx* ctx, FILE* out) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    bool daemon = true, parse_only = false;
+    bool daemon = true, parse_only = false, coalesce = false;
     int device = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--daemon=false") daemon = false;
         else if (a == "--parse-only") parse_only = true;
+        else if (a == "--coalesce") coalesce = true;   // graph_change_manager.go:220-229 optimizeChanges
         else if (a.rfind("--device=", 0) == 0) device = std::atoi(a.c_str() + 9);
         // the reference's other flags (--graph_has_node_types, --algorithm,
         // --print_assignments, --debug_output) need no action here
@@ -198,6 +201,12 @@ int main(int argc, char** argv) {
     bool first = true;
     while (read_iteration(stdin, first, s, lineno)) {
         if (!s.eoi) die("input ended inside an iteration (no 'c EOI')", lineno);
+        if (coalesce && !first) {
+            size_t kept = 0;
+            if (ks_coalesce_deltas(s.deltas.data(), s.deltas.size(), s.deltas.data(), s.deltas.size(), &kept) != KS_OK)
+                die("invalid node id in change records", lineno);
+            s.deltas.resize(kept);
+        }
         if (parse_only) {
             std::printf("iteration %s nodes %zu arcs %zu deltas %zu\n", first ? "full" : "incremental", s.nodes.size(),
                         s.arcs.size(), s.deltas.size());

@@ -424,6 +424,101 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     return KS_OK;
 }
 
+// Coalescing follows the store's semantics above: ADD_ARC and UPDATE_ARC are both
+// upserts of the full (low, cap, cost, type) and UPDATE_ARC 0/0 deletes, so the
+// last record of an arc decides its state (mergeChangesToSameArc and
+// removeDuplicateChanges); REMOVE_NODE drops every incident arc, so arc and
+// excess records touching the node before its removal are dead
+// (purgeChangesBeforeNodeRemoval). Survivors keep their relative order and a
+// kept record sits at its own position, after the ADD_NODEs of its endpoints.
+int ks_coalesce_deltas(const ks_delta* in, size_t k, ks_delta* out, size_t cap, size_t* count) {
+    if (!count || (k && !in) || k > (size_t)INT32_MAX) return KS_E_INVALID;
+    for (size_t i = 0; i < k; ++i) {             // ids as the store accepts them (hash keys ≠ 0)
+        const ks_delta& x = in[i];
+        const bool arc = x.kind == KS_ADD_ARC || x.kind == KS_UPDATE_ARC;
+        const uint64_t a = arc ? x.src : x.id, b = arc ? x.dst : 1;
+        if (a == 0 || b == 0 || a >= kMaxId || b >= kMaxId) return KS_E_INVALID;
+    }
+    std::vector<uint8_t> keep(k, 1);
+    ArcIndex last_arc;                           // (src, dst) → index of its live record
+    last_arc.reserve(k);
+    // node id → slot: direct when ids are dense (the FIFO-reused ids of a cell), else hashed
+    uint64_t max_id = 0;
+    for (size_t i = 0; i < k; ++i) {
+        const ks_delta& x = in[i];
+        const bool arc = x.kind == KS_ADD_ARC || x.kind == KS_UPDATE_ARC;
+        max_id = std::max(max_id, arc ? std::max(x.src, x.dst) : x.id);
+    }
+    const bool direct = max_id <= 4 * (uint64_t)k + 65536;
+    ArcIndex slot_of;                            // sparse ids: id → slot (key (id, 0))
+    std::vector<int> head(direct ? max_id + 1 : 0, -1);   // slot → newest record touching it
+    std::vector<int> last_exc(direct ? max_id + 1 : 0, -1);  // slot → live SET_EXCESS record
+    std::vector<int> link(2 * k, -1);            // record i: next older record at src (2i) / dst (2i+1)
+    auto slot = [&](uint64_t id) -> int {
+        if (direct) return (int)id;
+        int s = slot_of.find(arc_key(id, 0));
+        if (s < 0) {
+            s = (int)head.size();
+            slot_of.insert(arc_key(id, 0), s);
+            head.push_back(-1);
+            last_exc.push_back(-1);
+        }
+        return s;
+    };
+    // the list entry 2i+e belongs to node (e ? dst : src) of record i
+    auto push = [&](int s, int i, int e) {
+        link[2 * i + e] = head[s];
+        head[s] = 2 * i + e;
+    };
+    for (size_t i = 0; i < k; ++i) {
+        const ks_delta& x = in[i];
+        switch (x.kind) {
+            case KS_ADD_ARC:
+            case KS_UPDATE_ARC: {
+                const uint64_t key = arc_key(x.src, x.dst);
+                const int j = last_arc.find(key);
+                if (j >= 0) {
+                    keep[j] = 0;
+                    last_arc.erase(key);
+                }
+                last_arc.insert(key, (int)i);
+                push(slot(x.src), (int)i, 0);
+                if (x.dst != x.src) push(slot(x.dst), (int)i, 1);
+                break;
+            }
+            case KS_SET_EXCESS: {
+                const int s = slot(x.id);
+                if (last_exc[s] >= 0) keep[last_exc[s]] = 0;
+                last_exc[s] = (int)i;
+                break;
+            }
+            case KS_REMOVE_NODE: {
+                const int s = slot(x.id);
+                for (int e = head[s]; e >= 0; e = link[e]) {
+                    const int j = e >> 1;
+                    if (!keep[j]) continue;
+                    keep[j] = 0;
+                    last_arc.erase(arc_key(in[j].src, in[j].dst));
+                }
+                head[s] = -1;
+                if (last_exc[s] >= 0) keep[last_exc[s]] = 0;
+                last_exc[s] = -1;
+                break;
+            }
+            default:
+                break;                           // ADD_NODE and unknown kinds pass through
+        }
+    }
+    size_t n = 0;
+    for (size_t i = 0; i < k; ++i) {
+        if (!keep[i]) continue;
+        if (out && n < cap) out[n] = in[i];      // n ≤ i: in-place (out == in) is safe
+        ++n;
+    }
+    *count = n;
+    return KS_OK;
+}
+
 int ks_solve(ks_ctx* c, ks_result* out) {
     if (!c) return KS_E_INVALID;
     ks_result r;

@@ -19,6 +19,7 @@ KS_ADD_NODE, KS_REMOVE_NODE, KS_ADD_ARC, KS_UPDATE_ARC, KS_SET_EXCESS = 0, 1, 2,
 EXPORTED_SYMBOLS = (
     "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
     "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
+    "ks_coalesce_deltas",
 )
 
 NODE_DT = np.dtype({"names": ["id", "excess", "type", "_pad"],
@@ -106,6 +107,7 @@ def load(build_if_missing: bool = True):
     L.ks_get_task_mapping.argtypes = [V, V, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_task_pu_device.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
     L.ks_solve_many.argtypes = [P(V), C.c_size_t, C.c_int, P(KsResult)]
+    L.ks_coalesce_deltas.argtypes = [V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]
     _LIB = L
     return L
 
@@ -220,3 +222,15 @@ def solve_many(ctxs: list[Context], workers: int = 0) -> list[SolveResult]:
         bad = next(c for c, r in zip(ctxs, rs) if r.status != KS_OK)
         bad._check(rc)
     return [SolveResult(r.total_cost, r.flow_value, r.as_dict()) for r in rs[:k]]
+
+
+def coalesce_deltas(deltas: np.ndarray) -> np.ndarray:
+    """ks_coalesce_deltas: the change optimisers of graph_change_manager.go:220-279
+    (merge per arc, drop duplicates, purge before node removal). Host-only."""
+    d = np.ascontiguousarray(deltas, DELTA_DT)
+    out = np.zeros(d.shape[0], DELTA_DT)
+    cnt = C.c_size_t()
+    rc = load().ks_coalesce_deltas(d.ctypes.data, d.shape[0], out.ctypes.data, d.shape[0], C.byref(cnt))
+    if rc != KS_OK:
+        raise KsError(rc, "ks_coalesce_deltas: invalid node id in delta stream")
+    return out[:cnt.value]

@@ -48,3 +48,23 @@ def test_daemon_false_stops_after_first_graph(daemon):
 def test_malformed_input_fails_loudly(daemon, bad):
     p = run(daemon, bad)
     assert p.returncode != 0 and "ks_flow_scheduler" in p.stderr
+
+
+def test_coalesce_flag_matches_the_c_abi(daemon):
+    """--coalesce: each change block goes through ks_coalesce_deltas before it is
+    applied (optimizeChanges, graph_change_manager.go:220-229)."""
+    import numpy as np
+    from ksched_amd import native
+    cell = churn.Cell(300, 30, 3, 5, 7)
+    g = cell.graph()
+    _, _, _, fl = ko.cost_scaling(g)
+    d1 = cell.step(flow_mapping(g, fl), done=0, arrive=20)
+    g1 = cell.graph()
+    _, _, _, fl1 = ko.cost_scaling(g1)
+    d2 = cell.step(flow_mapping(g1, fl1), done=30, arrive=10)
+    d = np.concatenate([d1, d2])
+    p = run(daemon, ko.export_dimacs(g) + dimacs_changes(d), "--coalesce")
+    assert p.returncode == 0, p.stderr
+    kept = native.coalesce_deltas(d).shape[0]
+    assert kept < d.shape[0]
+    assert p.stdout.splitlines()[1] == f"iteration incremental nodes 0 arcs 0 deltas {kept}"

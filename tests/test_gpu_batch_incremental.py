@@ -109,3 +109,31 @@ def test_warm_resolve_without_changes_and_cold_opt_out():
         c.solve()
         r2 = c.solve()
         assert r2.cost == cost and r2.raw["warm_started"] == 0
+
+
+def test_coalesced_stream_solves_like_the_raw_stream():
+    """ks_coalesce_deltas before ks_apply_deltas (graph_change_manager.go:220-279):
+    two config-4 rounds batched into one stream give the same device solution as
+    the raw stream, and as the oracle on the cell's full graph."""
+    cell = churn.Cell(10_000, 1_000, 25, 100, 5)
+    raw, co = native.Context(0), native.Context(0)
+    for c in (raw, co):
+        c.load_graph(cell.graph())
+    raw.solve()
+    mp = raw.task_mapping()
+    parts = []
+    for _ in range(2):
+        parts.append(cell.step(mp, done=500, arrive=500))
+        mp = {}
+    d = np.concatenate(parts)
+    c = native.coalesce_deltas(d)
+    assert c.shape[0] < d.shape[0]
+    raw.apply_deltas(d)
+    co.apply_deltas(c)
+    r1, r2 = raw.solve(), co.solve()
+    st, cost, flow, _ = ko.cost_scaling(cell.graph())
+    assert st == 0
+    assert (r1.cost, r1.flow) == (r2.cost, r2.flow) == (cost, flow)
+    assert r1.raw["n_arcs"] == r2.raw["n_arcs"]
+    raw.close()
+    co.close()
