@@ -83,7 +83,7 @@ typedef struct ks_opts {
     int32_t  verify;           /* run the on-device verifier after every solve (1)      */
     int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */
     int32_t  price_refine;     /* certify optimality early by price refinement (1)      */
-    int32_t  gu_interval;      /* sweeps between global price updates (default 32)      */
+    int32_t  gu_interval;      /* sweeps between global price updates (default 24)      */
     int32_t  warm_start;       /* 1: re-solve from the previous flow and prices after
                                   ks_apply_deltas; 0 (default): every solve from
                                   scratch (faster on config 4)      */
