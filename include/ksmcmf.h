@@ -32,9 +32,11 @@
  *     sink 3, machine 4, numa/socket/cache/core 5, other 0).
  *   - arcs are (src, dst, low, cap, cost, type); at most one arc per ordered
  *     (src, dst) pair (node.go:118-131). ADD_ARC on an existing pair upserts.
- *   - UPDATE_ARC with low == cap == 0 keeps a zero-capacity arc (ChangeArc,
- *     graph_change_manager.go:142-156; DeleteArc emits the same record,
- *     :184-193) — an arc with zero capacity carries no flow either way.
+ *   - UPDATE_ARC with low == cap == 0 REMOVES the arc (DeleteArc emits this
+ *     record, graph_change_manager.go:184-193; ChangeArc to 0/0, :142-156, keeps
+ *     a zero-capacity arc in the reference, which carries no flow either, so the
+ *     two are equivalent for the solve). A later ADD_ARC / UPDATE_ARC re-creates
+ *     it. The arc then no longer counts in n_arcs.
  *   - REMOVE_NODE drops every incident arc implicitly (the reference emits only
  *     "r id", graph_change_manager.go:129-139); the id may be reused later.
  *   - SET_EXCESS sets a node's supply explicitly (the sink's demand drifts in

@@ -1364,11 +1364,15 @@ __global__ void k_drain_all(DG g) {
     if (h < g.nheavy) drain_inbox(g, h);
 }
 
-__global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const long long* __restrict__ low,
-                              const long long* __restrict__ cap, const long long* __restrict__ cost,
-                              long long* __restrict__ flows, long long* __restrict__ part) {
+// Also measures the flow value from the resident flow: net inflow into the
+// demand nodes (supply < 0), Σ over arcs of f·[dst demand] − f·[src demand].
+__global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const int* __restrict__ src,
+                              const int* __restrict__ dst, const long long* __restrict__ supply,
+                              const long long* __restrict__ low, const long long* __restrict__ cap,
+                              const long long* __restrict__ cost, long long* __restrict__ flows,
+                              long long* __restrict__ part, long long* __restrict__ partf) {
     __shared__ long long sh[WPB];
-    long long csum = 0;
+    long long csum = 0, fsum = 0;
     int bad = 0;
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < g.m; i += (long long)gridDim.x * BLK) {
         const int p = fwd[i];
@@ -1379,15 +1383,14 @@ __global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const long long
         const long long fl = f + low[i];
         flows[i] = fl;
         csum += fl * cost[i];
+        if (supply[dst[i]] < 0) fsum += fl;
+        if (supply[src[i]] < 0) fsum -= fl;
     }
-    csum = wave_sum(csum);
-    const int w = threadIdx.x >> 6;
-    if (lane_id() == 0) sh[w] = csum;
-    __syncthreads();
+    csum = block_sum(csum, sh);
+    fsum = block_sum(fsum, sh);
     if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int i = 0; i < WPB; ++i) t += sh[i];
-        part[blockIdx.x] = t;
+        part[blockIdx.x] = csum;
+        partf[blockIdx.x] = fsum;
     }
     if (__any(bad) && lane_id() == 0) atomicOr(&g.ctl->verify_bad, 1);
 }
@@ -1913,7 +1916,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.n_arcs = m;
     if (n == 0) {
         res.total_cost = 0;
-        res.flow_value = 0;
+        res.flow_value = 0;   // no arcs: nothing flows
         s.solved = true;
         return KS_OK;
     }
@@ -1941,7 +1944,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     for (auto& b : s.cls_list) KS_CHECK(b.ensure(n));
     KS_CHECK(s.nsel.ensure(NGC + 1));
     KS_CHECK(s.flows.ensure(m));
-    KS_CHECK(s.part.ensure(4096));
+    KS_CHECK(s.part.ensure(2 * 4096));   // per-block cost sums, then flow-value sums
     KS_CHECK(s.first.ensure(n + 2 + 64 * NGC));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
@@ -2315,21 +2318,27 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // ------------------------------------------------------------ verify ---
     KS_CHECK(hipEventRecord(s.ev[6], st));
     const int vgrid = grid_for(m, 2048);
-    long long tot_cost = 0;
+    long long tot_cost = 0, tot_flow = 0;
     if (status == KS_OK) {
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
         if (m) {
             hipLaunchKernelGGL(k_verify_arcs, dim3(vgrid), dim3(BLK), 0, st, g, (const int*)s.fwd.p,
+                               (const int*)s.a_src.p, (const int*)s.a_dst.p, (const long long*)s.supply.p,
                                (const long long*)s.a_low.p, (const long long*)s.a_cap.p,
-                               (const long long*)s.a_cost.p, s.flows.p, s.part.p);
+                               (const long long*)s.a_cost.p, s.flows.p, s.part.p, s.part.p + 4096);
             hipLaunchKernelGGL(k_verify_opt, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         }
         hipLaunchKernelGGL(k_verify_nodes, dim3(ngrid), dim3(BLK), 0, st, g);
-        std::vector<long long> parts(m ? vgrid : 0);
-        if (m) KS_CHECK(hipMemcpyAsync(parts.data(), s.part.p, vgrid * sizeof(long long), hipMemcpyDeviceToHost, st));
+        std::vector<long long> parts(m ? vgrid : 0), partf(m ? vgrid : 0);
+        if (m) {
+            KS_CHECK(hipMemcpyAsync(parts.data(), s.part.p, vgrid * sizeof(long long), hipMemcpyDeviceToHost, st));
+            KS_CHECK(hipMemcpyAsync(partf.data(), s.part.p + 4096, vgrid * sizeof(long long), hipMemcpyDeviceToHost,
+                                    st));
+        }
         KS_CHECK(read_ctl());
         for (long long x : parts) tot_cost += x;
+        for (long long x : partf) tot_flow += x;
         if (s.h_ctl->verify_bad && s.opts.verify) {
             status = KS_E_VERIFY;
             err = std::string("on-device verification failed (") +
@@ -2379,6 +2388,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
     }
     res.total_cost = tot_cost;
+    res.flow_value = tot_flow;
     res.phases = phases;
     res.sweeps = sweeps;
     res.arc_scans = tc[C_SCAN];

@@ -132,7 +132,8 @@ struct ks_ctx {
     std::vector<ArcRec> arcs;
     std::vector<int> free_arcs;
     ArcIndex arc_of;
-    std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy)
+    std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy, see push_incident)
+    std::vector<uint32_t> live_deg;        // per node: live incident arcs
     bool dirty = true;
     bool reloaded = true;                  // ks_load_graph since the last solve: no warm start
 
@@ -159,6 +160,7 @@ void ensure_node(ks_ctx* c, uint64_t id) {
     if (id >= c->nodes.size()) {
         c->nodes.resize(id + 1);
         c->inc.resize(id + 1);
+        c->live_deg.resize(id + 1, 0);
     }
 }
 
@@ -171,6 +173,27 @@ void kill_arc(ks_ctx* c, int slot) {
     a.prev_up = -1;
     c->arc_of.erase(arc_key(a.src, a.dst));
     c->free_arcs.push_back(slot);
+    --c->live_deg[a.src];
+    --c->live_deg[a.dst];
+}
+
+// Incidence lists are append-only between compactions: a killed arc's slot stays
+// in both endpoints' lists (and may later be reused by an arc of other nodes).
+// Long-lived hubs (sink, aggregators) would otherwise grow with history, so a
+// list is compacted to its live arcs once it exceeds twice its live degree.
+void push_incident(ks_ctx* c, uint64_t v, int slot) {
+    std::vector<int>& l = c->inc[v];
+    if (l.size() >= 2 * (size_t)c->live_deg[v] + 16) {
+        size_t k = 0;
+        for (int t : l) {
+            const ArcRec& a = c->arcs[t];
+            if (a.alive && (a.src == v || a.dst == v)) l[k++] = t;
+        }
+        l.resize(k);
+        std::sort(l.begin(), l.end());
+        l.erase(std::unique(l.begin(), l.end()), l.end());
+    }
+    l.push_back(slot);
 }
 
 int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int64_t cost, int32_t type) {
@@ -192,8 +215,11 @@ int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int6
         }
         c->arc_of.insert(arc_key(s, d), slot);
         c->arcs[slot].prev_up = -1;
-        c->inc[s].push_back(slot);
-        c->inc[d].push_back(slot);
+        c->arcs[slot].alive = false;       // not yet: compaction below must skip it
+        push_incident(c, s, slot);
+        push_incident(c, d, slot);
+        ++c->live_deg[s];
+        ++c->live_deg[d];
     }
     ArcRec& a = c->arcs[slot];
     a.src = s;
@@ -222,6 +248,7 @@ int remove_node(ks_ctx* c, uint64_t id) {
         if (a.alive && (a.src == id || a.dst == id)) kill_arc(c, slot);
     }
     c->inc[id].clear();
+    c->live_deg[id] = 0;
     c->nodes[id] = NodeRec{};
     return KS_OK;
 }
@@ -326,6 +353,7 @@ ks_ctx* ks_create(int device, const ks_opts* opts) {
     }
     c->nodes.resize(1);
     c->inc.resize(1);
+    c->live_deg.resize(1, 0);
     return c;
 }
 
@@ -338,6 +366,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     if ((n && !nodes) || (m && !arcs)) return c->fail(KS_E_INVALID, "null input array");
     c->nodes.assign(1, NodeRec{});
     c->inc.assign(1, {});
+    c->live_deg.assign(1, 0);
     c->arcs.clear();
     c->free_arcs.clear();
     c->arc_of.clear();
@@ -351,6 +380,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     if (maxid < kMaxId) {
         c->nodes.reserve(maxid + 1);
         c->inc.reserve(maxid + 1);
+        c->live_deg.reserve(maxid + 1);
     }
     for (size_t i = 0; i < n; ++i) {
         int rc = add_node(c, nodes[i].id, nodes[i].excess, nodes[i].type);
@@ -398,6 +428,10 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
                 rc = upsert_arc(c, x.src, x.dst, (int64_t)x.low, (int64_t)x.cap, x.cost, x.type);
                 break;
             case KS_UPDATE_ARC: {
+                if (x.src == 0 || x.dst == 0 || x.src >= kMaxId || x.dst >= kMaxId) {
+                    rc = c->fail(KS_E_RANGE, "arc endpoint id out of range");
+                    break;
+                }
                 if (x.low == 0 && x.cap == 0) {  // DeleteArc / ChangeArc(0,0): no capacity left
                     const int slot = c->arc_of.find(arc_key(x.src, x.dst));
                     if (slot >= 0) kill_arc(c, slot);
@@ -533,11 +567,7 @@ int ks_solve(ks_ctx* c, ks_result* out) {
         for (size_t i = 0; i < c->up_arc.size(); ++i) c->arcs[c->up_arc[i]].prev_up = (int)i;
         for (auto& nd : c->nodes) nd.fresh = false;
         c->reloaded = false;
-        int64_t pos = 0;
-        for (int64_t v : c->c_supply)
-            if (v > 0) pos += v;
-        r.flow_value = pos;
-        c->have_solution = true;
+        c->have_solution = true;   // r.flow_value: measured on device from the resident flow
     }
     r.status = rc;
     if (out) *out = r;

@@ -219,7 +219,9 @@ def solve_many(ctxs: list[Context], workers: int = 0) -> list[SolveResult]:
     rs = (KsResult * max(1, k))()
     rc = L.ks_solve_many(hs, k, workers, rs)
     if rc != KS_OK:
-        bad = next(c for c, r in zip(ctxs, rs) if r.status != KS_OK)
+        bad = next((c for c, r in zip(ctxs, rs) if r.status != KS_OK), None)
+        if bad is None:   # rejected before any solve ran (e.g. a null context)
+            raise KsError(rc, "ks_solve_many failed")
         bad._check(rc)
     return [SolveResult(r.total_cost, r.flow_value, r.as_dict()) for r in rs[:k]]
 

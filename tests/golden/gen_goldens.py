@@ -8,6 +8,8 @@ in the build container). networkx never travels to the GPU box: there the
 graphs are regenerated from (params, seed) and checked against these numbers.
 
 ``--big`` also solves the config-3 graph (100k tasks × 10k machines, ≈15 min).
+``--batch64`` adds all 64 config-5 cells (config-2 graphs, seeds 1000..1063),
+solved in parallel worker processes (≈9 s each).
 """
 from __future__ import annotations
 
@@ -15,6 +17,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ProcessPoolExecutor
 
 import networkx as nx
 
@@ -41,6 +44,17 @@ def nx_solve(g):
     return int(cost) + const, flow
 
 
+def solve_case(case):
+    fam, params, seed = case
+    g = gen.trivial(*params) if fam == "trivial" else gen.quincy(*params, seed)
+    t0 = time.time()
+    cost, flow = nx_solve(g)
+    dt = time.time() - t0
+    print(f"{fam} {params} seed={seed}: n={g.n} m={g.m} cost={cost} flow={flow} ({dt:.1f}s)", flush=True)
+    return {"family": fam, "params": list(params), "seed": seed, "n": g.n, "m": g.m,
+            "cost": cost, "flow": flow, "solver": f"networkx {nx.__version__} network_simplex"}
+
+
 def main():
     big = "--big" in sys.argv
     cases = []
@@ -61,24 +75,22 @@ def main():
         cases.append(("quincy", gen.CONFIGS["config2"][:4], seed))
     if big:
         cases.append(("quincy", gen.CONFIGS["config3"][:4], gen.CONFIGS["config3"][4]))
+    if "--batch64" in sys.argv:      # config 5: 64 config-2 cells, seeds 1000..1063
+        for seed in range(1004, 1064):
+            cases.append(("quincy", gen.CONFIGS["config2"][:4], seed))
 
     old = {}
     if os.path.exists(OUT):
         for e in json.load(open(OUT))["graphs"]:
             old[(e["family"], tuple(e["params"]), e["seed"])] = e
+    todo = [c for c in cases if (c[0], tuple(c[1]), c[2]) not in old]
+    workers = int(os.environ.get("GOLDEN_WORKERS", "6"))
+    with ProcessPoolExecutor(max(1, workers)) as ex:
+        fresh = dict(zip(todo, ex.map(solve_case, todo)))
     res = []
     for fam, params, seed in cases:
         key = (fam, tuple(params), seed)
-        if key in old:
-            res.append(old[key])
-            continue
-        g = gen.trivial(*params) if fam == "trivial" else gen.quincy(*params, seed)
-        t0 = time.time()
-        cost, flow = nx_solve(g)
-        dt = time.time() - t0
-        print(f"{fam} {params} seed={seed}: n={g.n} m={g.m} cost={cost} flow={flow} ({dt:.1f}s)", flush=True)
-        res.append({"family": fam, "params": list(params), "seed": seed, "n": g.n, "m": g.m,
-                    "cost": cost, "flow": flow, "solver": f"networkx {nx.__version__} network_simplex"})
+        res.append(old[key] if key in old else fresh[(fam, params, seed)])
     for k, e in old.items():
         if all((r["family"], tuple(r["params"]), r["seed"]) != k for r in res):
             res.append(e)

@@ -135,3 +135,45 @@ def random_graphs(seed: int, count: int, max_n: int = 60, cost_lo: int = 0, cost
             supply[b] -= k
         nodes = [(i + 1, int(supply[i]), 0) for i in range(n)]
         yield trial, graph_from_lists(nodes, arcs)
+
+
+def parse_dimacs(text: str):
+    """ksched's solver wire text (dimacs/export.go:11-76 for a full graph,
+    dimacs/*_change.go GenerateChange for an incremental block) →
+    (nodes [(id, excess, type)], arcs [(src, dst, low, cap, cost)], deltas DELTA_DT).
+    A full export yields nodes/arcs, a change block yields delta records."""
+    from ksched_amd import native
+    nodes, arcs, recs = [], [], []
+    for line in text.splitlines():
+        f = line.split()
+        if not f or f[0] in ("c", "p"):
+            continue
+        v = [int(x) for x in f[1:]]
+        if f[0] == "n":
+            nodes.append(tuple(v))
+            recs.append(dict(kind=native.KS_ADD_NODE, id=v[0], excess=v[1], type=v[2]))
+        elif f[0] == "a":
+            arcs.append(tuple(v[:5]))
+            recs.append(dict(kind=native.KS_ADD_ARC, src=v[0], dst=v[1], low=v[2], cap=v[3], cost=v[4],
+                             type=v[5] if len(v) > 5 else 0))
+        elif f[0] == "x":
+            recs.append(dict(kind=native.KS_UPDATE_ARC, src=v[0], dst=v[1], low=v[2], cap=v[3], cost=v[4],
+                             type=v[5], old_cost=v[6] if len(v) > 6 else 0))
+        elif f[0] == "r":
+            recs.append(dict(kind=native.KS_REMOVE_NODE, id=v[0]))
+        else:
+            raise ValueError(f"unknown DIMACS record {line!r}")
+    d = np.zeros(len(recs), native.DELTA_DT)
+    for i, x in enumerate(recs):
+        for k, val in x.items():
+            d[i][k] = val
+    return nodes, arcs, d
+
+
+def load_multi_schedule():
+    """tests/golden/multi_schedule_iteration.json (gen_multi_schedule.py)."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multi_schedule_iteration.json")
+    with open(p) as f:
+        return json.load(f)["rounds"]

@@ -137,3 +137,53 @@ def test_coalesced_stream_solves_like_the_raw_stream():
     assert r1.raw["n_arcs"] == r2.raw["n_arcs"]
     raw.close()
     co.close()
+
+
+def test_config4_full_size_rounds():
+    """Config 4 at its stated size: the config-3 cell (100k tasks,
+    10k machines, seed 3) under 5 % completions + 5 % arrivals per round, pins,
+    ageing and capacity refresh, three rounds through ks_apply_deltas. Every
+    round: bit-exact cost vs the cost-scaling oracle on the cell's full graph,
+    the oracle's verifier accepts the downloaded flow, and every running task
+    stays on its PU (graph_manager.go:675-720 pinning, :803-813 removal)."""
+    T, M, R, J, seed = gen.CONFIGS["config3"]
+    cell = churn.Cell(T, M, R, J, seed)
+    with native.Context(0) as ctx:
+        ctx.load_graph(cell.graph())
+        ctx.solve()
+        mp = ctx.task_mapping()
+        for rnd in range(3):
+            d = cell.step(mp, done=T // 20, arrive=T // 20)
+            ctx.apply_deltas(d)
+            r = ctx.solve()
+            g = cell.graph()
+            st, cost, flow, _ = ko.cost_scaling(g)
+            assert st == 0
+            assert (r.cost, r.flow) == (cost, flow), f"round {rnd + 1}"
+            fl = flows_by_arc(ctx, g)
+            vst, vcost, _ = ko.verify(g, fl)
+            assert vst == 0 and vcost == cost
+            mp = ctx.task_mapping()
+            check_mapping(g, mp)
+            run = cell.task_ids(cell.RUN)
+            assert all(mp[int(t)] == int(cell.pu[int(t) - cell.TASK0]) for t in run.tolist())
+
+
+def test_config5_full_batch_vs_goldens(ctx):
+    """Config 5 at its stated size: all 64 config-2 cells (seeds 1000..1063) as
+    one device solve of their disjoint union; every per-cell cost (from the flow
+    records) equals its committed networkx golden."""
+    from conftest import load_goldens
+    from ksched_amd import batch
+    T, M, R, J, _ = gen.CONFIGS["config2"]
+    gold = {e["seed"]: e for e in load_goldens() if e["params"] == [T, M, R, J]}
+    seeds = list(range(1000, 1064))
+    assert all(s in gold for s in seeds), "missing config-5 goldens (gen_goldens.py --batch64)"
+    graphs = [gen.quincy(T, M, R, J, s) for s in seeds]
+    u, noff, _ = batch.union(graphs)
+    ctx.load_graph(u)
+    r = ctx.solve()
+    assert r.flow == 64 * T
+    per = batch.split_costs(u, noff, ctx.flows())
+    assert per.tolist() == [gold[s]["cost"] for s in seeds]
+    assert r.cost == sum(gold[s]["cost"] for s in seeds)
