@@ -1,10 +1,10 @@
 // ks_engine.h — device engine of libksmcmf (gfx950). Internal to the library:
 // the public boundary is include/ksmcmf.h.
 //
-// The engine owns one solve's device state: the input arc arrays (uploaded by
-// the host graph store), the residual CSR built from them on device, the
-// node state (excess, double-buffered prices) and the control block the host
-// polls between kernel batches. See DESIGN.md §3-§4 for the algorithm.
+// The engine owns the device-resident graph (ks_store.h: node store, arc table,
+// hash index, residual CSR with slack), the solver state (excess,
+// double-buffered prices, frontiers) and the control block the host polls
+// between kernel batches. See DESIGN.md §3-§4 for the algorithm.
 #pragma once
 
 #include <cstdint>
@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/ksmcmf.h"
+#include "ks_store.h"
 
 namespace ks {
 
@@ -26,35 +27,38 @@ public:
 
     int init(int device, const ks_opts& opts, std::string& err);
 
-    // Copy a compacted graph (0-based node slots) into device input arrays.
-    // supply[n] is the node excess after any auto-sink adjustment. For a warm
-    // start, prev_idx[m] gives each arc's index in the previous upload (−1 = new)
-    // and fresh[n] marks node slots created since the previous solve; both may
-    // be null (no warm start for this graph).
-    int upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst,
-               const int64_t* low, const int64_t* cap, const int64_t* cost,
-               const int64_t* supply, const uint8_t* type, const int32_t* prev_idx,
-               const uint8_t* fresh, std::string& err);
+    // Replace the device store: node slots [0, nslots) (slot = NodeID − 1) with
+    // their supply, DIMACS type and liveness, and the arcs (1-based ids, already
+    // validated; a repeated (src, dst) pair: the last one wins).
+    int load(int64_t nslots, const int64_t* supply, const uint8_t* type, const uint8_t* alive, const ks_arc* arcs,
+             size_t m, std::string& err);
 
-    // Build the residual CSR on device and run ε-scaling push-relabel to
-    // optimality, then verify on device. Fills r (never NULL here).
-    // warm: start from the previous solution when one maps onto this graph.
+    // Apply a validated delta stream on the device (ks_store.h): the final state
+    // of every node it touches plus the raw records; nslots = node slots in use.
+    int apply(const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t k, int64_t nslots, std::string& err);
+
+    // Node state changes outside a stream (the auto-sink demand).
+    int set_nodes(const NodeEdit* edits, size_t ne, std::string& err);
+
+    // ε-scaling push-relabel to optimality on the device-resident graph, then
+    // on-device verification. Fills r. warm: start from the flow and prices in
+    // place (the previous solve's, edited by the deltas since).
     int solve(ks_result& r, bool warm, std::string& err);
 
-    // Flow on every input arc (input order) from the last successful solve.
-    int download_flows(int64_t* flows, std::string& err);
+    // Arcs with positive flow in the last solve (the "f" lines), arc-slot order.
+    int flows(std::vector<ks_flow>& out, std::string& err);
 
     // Task → PU placement of the last solve, decomposed on device: for the i-th
-    // task slot (DIMACS type 1) in slot order, the node id (slot + 1) of the last
-    // PU its flow unit crosses, 0 when unscheduled. *count = number of tasks;
-    // dev_out (device memory, ≥ count entries) may be null to query the count.
-    int task_pu(uint64_t* dev_out, size_t cap, size_t* count, std::string& err);
+    // live task slot in slot order, the node id of the last PU its flow unit
+    // crosses, 0 when unscheduled. *count = n_tasks; dev_out (device memory,
+    // ≥ n_tasks entries) may be null to query the count.
+    int task_pu(uint64_t* dev_out, size_t cap, size_t* count, int64_t n_tasks, std::string& err);
 
     // Engine-owned device scratch of n uint64 (valid until the next call).
     int scratch(uint64_t** dev, size_t n, std::string& err);
     int download(void* host_dst, const void* dev_src, size_t bytes, std::string& err);
 
-
+    int64_t live_arcs() const;
     int device() const;
 
 private:

@@ -80,7 +80,6 @@ constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
-constexpr long long kTraceMax = 1 << 16;   // sweeps recorded when KS_TRACE is set
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5 };
 
@@ -154,9 +153,6 @@ struct DG {
     Front bf[3];   // Bellman-Ford frontiers
     Ctl* ctl;
     unsigned long long* ctr;
-    unsigned* trace;   // optional per-sweep [visits, relabels, groups, heavy] (KS_TRACE)
-    unsigned long long* stamps;   // optional per-block [t0, t1, kind|active] of one sweep (KS_STAMP)
-    int stamp_sweep;
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -430,59 +426,46 @@ __device__ __forceinline__ int wave_index_in_grid(int first_block) {
 }
 
 // ===================================================================== build ===
-__global__ void k_make_keys(int m, const int* __restrict__ src, const int* __restrict__ dst,
-                            const int* __restrict__ perm, unsigned* __restrict__ keys, int* __restrict__ vals) {
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
-        const int s = src[i], d = dst[i];
-        keys[2 * i] = (unsigned)(perm ? perm[s] : s);
-        keys[2 * i + 1] = (unsigned)(perm ? perm[d] : d);
-        if (vals) {
-            vals[2 * i] = (int)(2 * i);
-            vals[2 * i + 1] = (int)(2 * i + 1);
+// The residual CSR is built on device from the arc table of the store
+// (ks_store.h). Every node owns a segment of CAPACITY positions: its live arcs
+// (forward arcs and reverses of its in-arcs), plus slack once the graph is
+// edited incrementally, so later inserts land in place. Internal ids group the
+// nodes by the degree class of their capacity, hubs last; dead positions are
+// inert (no capacity, head = owner, cost DEAD_COST).
+__global__ void k_degree(int hi, const unsigned char* __restrict__ alive, const int* __restrict__ src,
+                         const int* __restrict__ dst, int* __restrict__ deg) {
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK)
+        if (alive[s]) {
+            atomicAdd(&deg[src[s]], 1);
+            atomicAdd(&deg[dst[s]], 1);
         }
+}
+
+// Segment capacity of a node slot: its degree; with slack (incremental mode)
+// +25 % (at least 2) rounded up to a lane group (≤ 64) or a 64-arc chunk, and
+// one 8-lane group for dead or spare slots (room for a task id that is reused,
+// flowgraph/graph.go:169-182).
+__host__ __device__ inline int seg_capacity(int deg, bool alive, int slack) {
+    if (!slack) return deg;
+    if (!alive && deg == 0) return 8;
+    const int c = deg + (deg / 4 > 2 ? deg / 4 : 2);
+    if (c <= 64) {
+        int g = 4;
+        while (g < c) g <<= 1;
+        return g;
     }
+    return (c + 63) / 64 * 64;
 }
 
-__global__ void k_scatter_pos(long long m2, const int* __restrict__ vals, int* __restrict__ pos_of) {
-    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK)
-        pos_of[vals[p]] = (int)p;
-}
-
-__global__ void k_fill(long long m2, long long mult, const int* __restrict__ vals, const int* __restrict__ pos_of,
-                       const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
-                       const long long* __restrict__ low, const long long* __restrict__ cap,
-                       const long long* __restrict__ cost, int* __restrict__ head, int* __restrict__ rev,
-                       long long* __restrict__ rcap, long long* __restrict__ ucap, long long* __restrict__ scost,
-                       int* __restrict__ fwd) {
-    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
-        const int v = vals[p];
-        const int i = v >> 1;
-        const bool r = v & 1;
-        head[p] = perm[r ? src[i] : dst[i]];
-        rev[p] = pos_of[v ^ 1];
-        const long long u = cap[i] - low[i];
-        rcap[p] = r ? 0 : u;
-        ucap[p] = u;
-        scost[p] = (r ? -cost[i] : cost[i]) * mult;
-        if (!r) fwd[i] = (int)p;
+__global__ void k_capacity(int ncap, int nstore, const int* __restrict__ deg, const unsigned char* __restrict__ alive,
+                           int slack, int* __restrict__ capv, unsigned char* __restrict__ cls) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
+        const int d = v < nstore ? deg[v] : 0;
+        const bool a = v < nstore && alive[v];
+        const int c = seg_capacity(d, a, slack);
+        capv[v] = c;
+        cls[v] = (unsigned char)degree_class(c);
     }
-}
-
-// first[v] = lower bound of v in the sorted keys, v ∈ [0, nn].
-__global__ void k_first(int nn, long long m2, const unsigned* __restrict__ keys, int* __restrict__ first) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v <= nn; v += (long long)gridDim.x * BLK) {
-        long long lo = 0, hi = m2;
-        while (lo < hi) {
-            const long long mid = (lo + hi) >> 1;
-            if (keys[mid] < (unsigned)v) lo = mid + 1; else hi = mid;
-        }
-        first[v] = (int)lo;
-    }
-}
-
-__global__ void k_classify(int n, const int* __restrict__ first, unsigned char* __restrict__ cls) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
-        cls[v] = (unsigned char)degree_class(first[v + 1] - first[v]);
 }
 
 // perm[list[i]] = base + i (one class, or the hubs).
@@ -491,32 +474,139 @@ __global__ void k_make_perm(int cnt, int base, const int* __restrict__ list, int
         perm[list[i]] = base + (int)i;
 }
 
-__global__ void k_node_init(int nn, long long* __restrict__ excess, long long* __restrict__ p0,
-                            long long* __restrict__ p1) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < nn; v += (long long)gridDim.x * BLK) {
-        excess[v] = 0;
-        p0[v] = 0;
-        p1[v] = 0;
+__global__ void k_capi(int ncap, const int* __restrict__ perm, const int* __restrict__ capv, int* __restrict__ capi,
+                       int* __restrict__ iperm) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
+        capi[perm[v]] = capv[v];
+        iperm[perm[v]] = (int)v;
     }
 }
 
-// excess[perm[v]] = supply[v]; then the lower-bound transform per arc.
-__global__ void k_supply(int n, const long long* __restrict__ supply, const int* __restrict__ perm,
-                         long long* __restrict__ excess) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
-        excess[perm[v]] = supply[v];
+// Sort keys: the tail (internal id) of every residual arc; dead slots sort last.
+__global__ void k_pos_keys(int hi, int sentinel, const unsigned char* __restrict__ alive, const int* __restrict__ src,
+                           const int* __restrict__ dst, const int* __restrict__ perm, unsigned* __restrict__ keys,
+                           int* __restrict__ vals) {
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
+        const bool a = alive[s];
+        keys[2 * s] = a ? (unsigned)perm[src[s]] : (unsigned)sentinel;
+        keys[2 * s + 1] = a ? (unsigned)perm[dst[s]] : (unsigned)sentinel;
+        vals[2 * s] = (int)(2 * s);
+        vals[2 * s + 1] = (int)(2 * s + 1);
+    }
 }
 
-__global__ void k_lower_bounds(int m, const int* __restrict__ src, const int* __restrict__ dst,
-                               const int* __restrict__ perm, const long long* __restrict__ low,
-                               long long* __restrict__ excess) {
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
-        const long long l = low[i];
-        if (l) {
-            atom_add(&excess[perm[src[i]]], -l);
-            atom_add(&excess[perm[dst[i]]], l);
+// rs[v] = lower bound of v in the sorted keys, v ∈ [0, nn].
+__global__ void k_first(int nn, long long m2, const unsigned* __restrict__ keys, int* __restrict__ rs) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v <= nn; v += (long long)gridDim.x * BLK) {
+        long long lo = 0, hi = m2;
+        while (lo < hi) {
+            const long long mid = (lo + hi) >> 1;
+            if (keys[mid] < (unsigned)v) lo = mid + 1; else hi = mid;
+        }
+        rs[v] = (int)lo;
+    }
+}
+
+// Every position inert, owned by the node whose segment holds it.
+__global__ void k_inert_all(long long m2cap, int nn, const int* __restrict__ first, int* __restrict__ head,
+                            int* __restrict__ rev, int* __restrict__ ent, long long* __restrict__ rcap,
+                            long long* __restrict__ ucap, long long* __restrict__ scost) {
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2cap; p += (long long)gridDim.x * BLK) {
+        int lo = 0, hi = nn;   // owner: the last v with first[v] <= p
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (first[mid] <= p) lo = mid; else hi = mid;
+        }
+        head[p] = lo;
+        rev[p] = (int)p;
+        ent[p] = -1;
+        rcap[p] = 0;
+        ucap[p] = 0;
+        scost[p] = DEAD_COST;
+    }
+}
+
+__global__ void k_fill_csr(long long m2, int nn, const unsigned* __restrict__ keys, const int* __restrict__ vals,
+                           const int* __restrict__ rs, const int* __restrict__ first, const int* __restrict__ perm,
+                           const int* __restrict__ src, const int* __restrict__ dst, const long long* __restrict__ low,
+                           const long long* __restrict__ cap, const long long* __restrict__ cost, long long mult,
+                           int* __restrict__ head, long long* __restrict__ rcap, long long* __restrict__ ucap,
+                           long long* __restrict__ scost, int* __restrict__ ent, int* __restrict__ fwd,
+                           int* __restrict__ pos_of) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m2; i += (long long)gridDim.x * BLK) {
+        const int v = (int)keys[i];
+        if (v >= nn) continue;
+        const int p = first[v] + (int)(i - rs[v]);
+        const int val = vals[i];
+        const int s = val >> 1;
+        const bool r = val & 1;
+        pos_of[val] = p;
+        head[p] = perm[r ? src[s] : dst[s]];
+        const long long u = cap[s] - low[s];
+        rcap[p] = r ? 0 : u;
+        ucap[p] = u;
+        scost[p] = (r ? -cost[s] : cost[s]) * mult;
+        ent[p] = val;
+        if (!r) fwd[s] = p;
+    }
+}
+
+__global__ void k_fill_rev(long long m2, int nn, const unsigned* __restrict__ keys, const int* __restrict__ vals,
+                           const int* __restrict__ pos_of, int* __restrict__ rev) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m2; i += (long long)gridDim.x * BLK) {
+        if ((int)keys[i] >= nn) continue;
+        const int val = vals[i];
+        rev[pos_of[val]] = pos_of[val ^ 1];
+    }
+}
+
+__global__ void k_used(int nn, const int* __restrict__ rs, int* __restrict__ used) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < nn; v += (long long)gridDim.x * BLK)
+        used[v] = rs[v + 1] - rs[v];
+}
+
+// ------------------------------------------------------------ cold reset ---
+// Zero flow: forward residual = u, reverse 0; excess = supply with the
+// lower-bound transform; prices 0. Runs before every cold solve (no rebuild).
+__global__ void k_reset_pos(long long m2cap, const int* __restrict__ ent, const long long* __restrict__ ucap,
+                            long long* __restrict__ rcap) {
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2cap; p += (long long)gridDim.x * BLK) {
+        const int e = ent[p];
+        if (e >= 0) rcap[p] = (e & 1) ? 0 : ucap[p];
+    }
+}
+
+__global__ void k_reset_nodes(int nn, int ncap, const int* __restrict__ iperm, const unsigned char* __restrict__ alive,
+                              const long long* __restrict__ supply, long long* __restrict__ excess,
+                              long long* __restrict__ p0, long long* __restrict__ p1) {
+    for (long long x = blockIdx.x * (long long)BLK + threadIdx.x; x < nn; x += (long long)gridDim.x * BLK) {
+        const int v = iperm[x];
+        excess[x] = (v >= 0 && v < ncap && alive[v]) ? supply[v] : 0;
+        p0[x] = 0;
+        p1[x] = 0;
+    }
+}
+
+__global__ void k_reset_low(int hi, const unsigned char* __restrict__ alive, const int* __restrict__ src,
+                            const int* __restrict__ dst, const int* __restrict__ perm,
+                            const long long* __restrict__ low, long long* __restrict__ excess) {
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
+        const long long l = low[s];
+        if (alive[s] && l) {
+            atom_add(&excess[perm[src[s]]], -l);
+            atom_add(&excess[perm[dst[s]]], l);
         }
     }
+}
+
+// max |cost| over live arcs → *out (the first phase's ε).
+__global__ void k_max_cost(int hi, const unsigned char* __restrict__ alive, const long long* __restrict__ cost,
+                           long long* __restrict__ out) {
+    long long mx = 0;
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK)
+        if (alive[s]) mx = max(mx, cost[s] < 0 ? -cost[s] : cost[s]);
+    mx = wave_max(mx);
+    if (lane_id() == 0 && mx) __hip_atomic_fetch_max(out, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct ClassIs {
@@ -924,7 +1014,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
     }
 }
 
-__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx) {
+__global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
     if (!g.ctl->bf_done) return;   // the preceding global update has not been applied
@@ -933,8 +1023,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
     const long long eps = g.ctl->eps;
     const long long* P = (pos & 1) ? g.p1 : g.p0;
     long long* PN = (pos & 1) ? g.p0 : g.p1;
-    const bool stamp = g.stamps && tidx == g.stamp_sweep;
-    const unsigned long long ts0 = stamp ? __builtin_amdgcn_s_memrealtime() : 0;
     Pend pd{-1, 0};
     Cnt c;
     int out = 0;
@@ -966,27 +1054,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq, int tidx)
         }
     }
     if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
-    if (stamp) {
-        const int busy = __syncthreads_or(c.visit > 0 || c.scan > 0);
-        if (threadIdx.x == 0) {
-            const int w0 = wave_index_in_grid(g.nhitems);
-            int kind = (int)blockIdx.x < g.nhitems ? 7 : (w0 >= g.wbeg[CCLS] ? 6 : 0);
-            for (int k = 1; k <= CCLS && kind == 0; ++k)
-                if (w0 < g.wbeg[k]) kind = k;   // window class + 1
-            g.stamps[3 * blockIdx.x] = ts0;
-            g.stamps[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-            g.stamps[3 * blockIdx.x + 2] = (unsigned long long)kind | ((unsigned long long)busy << 8);
-        }
-    }
-    if (g.trace && tidx >= 0) {
-        const long long v = wave_sum(c.visit), r = wave_sum(c.relabel);
-        if (lane_id() == 0 && (v | r)) {
-            const int cls = (int)blockIdx.x < g.nhitems ? 3 : 2;
-            atomicAdd(&g.trace[4 * tidx], (unsigned)v);
-            atomicAdd(&g.trace[4 * tidx + 1], (unsigned)r);
-            atomicAdd(&g.trace[4 * tidx + cls], (unsigned)v);
-        }
-    }
     flush_counters(g, c);
 }
 
@@ -1364,18 +1431,29 @@ __global__ void k_drain_all(DG g) {
     if (h < g.nheavy) drain_inbox(g, h);
 }
 
-// Also measures the flow value from the resident flow: net inflow into the
-// demand nodes (supply < 0), Σ over arcs of f·[dst demand] − f·[src demand].
-__global__ void k_verify_arcs(DG g, const int* __restrict__ fwd, const int* __restrict__ src,
-                              const int* __restrict__ dst, const long long* __restrict__ supply,
-                              const long long* __restrict__ low, const long long* __restrict__ cap,
-                              const long long* __restrict__ cost, long long* __restrict__ flows,
-                              long long* __restrict__ part, long long* __restrict__ partf) {
+// Per live arc slot: flow (lower bound included) into flows[s], capacity
+// feasibility, the cost sum, and the flow value measured from the resident
+// flow: net inflow into the demand nodes (supply < 0).
+__global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ alive, const int* __restrict__ fwd,
+                              const int* __restrict__ src, const int* __restrict__ dst,
+                              const long long* __restrict__ supply, const long long* __restrict__ low,
+                              const long long* __restrict__ cap, const long long* __restrict__ cost,
+                              long long* __restrict__ flows, long long* __restrict__ part,
+                              long long* __restrict__ partf) {
     __shared__ long long sh[WPB];
     long long csum = 0, fsum = 0;
     int bad = 0;
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < g.m; i += (long long)gridDim.x * BLK) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < hi; i += (long long)gridDim.x * BLK) {
+        if (!alive[i]) {
+            flows[i] = 0;
+            continue;
+        }
         const int p = fwd[i];
+        if (p < 0) {
+            bad = 1;
+            flows[i] = 0;
+            continue;
+        }
         const long long cp = cap[i] - low[i];
         const long long rf = g.rcap[p], rr = g.rcap[g.rev[p]];
         const long long f = cp - rf;
@@ -1416,37 +1494,50 @@ __global__ void k_verify_nodes(DG g) {
 }
 
 // ======================================================== warm start ===
-// Incremental re-solve (config 4): the previous solve's flow on every arc that
-// survived the deltas (prev[i] = its index in the previous upload, −1 = new or
-// re-created; prev == nullptr: same arcs, same order) is re-applied, clamped
-// into the arc's current bounds; node imbalances become excess/deficit.
-__global__ void k_warm_flows(int m, const int* __restrict__ prev, const long long* __restrict__ pflows,
-                             const long long* __restrict__ low, const long long* __restrict__ cap,
-                             const int* __restrict__ fwd, const int* __restrict__ rev, long long* __restrict__ rcap,
-                             const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
-                             long long* __restrict__ excess) {
-    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m; i += (long long)gridDim.x * BLK) {
-        const int pi = prev ? prev[i] : (int)i;
-        if (pi < 0) continue;
-        const long long lo = low[i], c = cap[i];
-        long long f = pflows[pi];
-        f = (f < lo ? lo : (f > c ? c : f)) - lo;
+// Incremental re-solve (config 4). While the CSR stays valid the previous flow
+// and prices simply remain in place (the store's kernels keep the residual
+// state consistent with every delta). Across a rebuild they are carried by arc
+// slot and node slot: saved before, restored (clamped to the new bounds) after.
+__global__ void k_save_flows(int hi, const unsigned char* __restrict__ alive, const int* __restrict__ fwd,
+                             const int* __restrict__ rev, const long long* __restrict__ rcap,
+                             long long* __restrict__ saved) {
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
+        const int p = fwd[s];
+        saved[s] = (alive[s] && p >= 0) ? rcap[rev[p]] : 0;
+    }
+}
+
+__global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive, const long long* __restrict__ saved,
+                                const long long* __restrict__ low, const long long* __restrict__ cap,
+                                const int* __restrict__ fwd, const int* __restrict__ rev,
+                                const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
+                                long long* __restrict__ rcap, long long* __restrict__ excess) {
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
+        if (!alive[s]) continue;
+        const long long u = cap[s] - low[s];
+        long long f = saved[s];
+        f = f < 0 ? 0 : (f > u ? u : f);
         if (f > 0) {
-            const int p = fwd[i];
-            rcap[p] = (c - lo) - f;
+            const int p = fwd[s];
+            rcap[p] = u - f;
             rcap[rev[p]] = f;
-            atom_add(&excess[perm[src[i]]], -f);
-            atom_add(&excess[perm[dst[i]]], f);
+            atom_add(&excess[perm[src[s]]], -f);
+            atom_add(&excess[perm[dst[s]]], f);
         }
     }
 }
 
-// Previous prices by node slot (ids are stable), rescaled when the cost
-// multiplier n+1 changed; slots beyond the previous graph start at 0.
-__global__ void k_warm_prices(int n, int n_prev, long long mult_prev, long long mult,
-                              const long long* __restrict__ pslot, const int* __restrict__ perm,
-                              long long* __restrict__ p0, long long* __restrict__ p1) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+__global__ void k_save_prices(int ncap, const int* __restrict__ perm, const long long* __restrict__ p0,
+                              long long* __restrict__ pslot) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK)
+        pslot[v] = p0[perm[v]];
+}
+
+// Saved prices by node slot, rescaled when the cost multiplier changed.
+__global__ void k_restore_prices(int ncap, int n_prev, long long mult_prev, long long mult,
+                                 const long long* __restrict__ pslot, const int* __restrict__ perm,
+                                 long long* __restrict__ p0, long long* __restrict__ p1) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
         long long p = 0;
         if (v < n_prev) {
             const long long q = pslot[v];
@@ -1459,9 +1550,8 @@ __global__ void k_warm_prices(int n, int n_prev, long long mult_prev, long long 
 
 // Nodes created since the previous solve (fresh[v] = 1) get the lowest price
 // at which none of their residual out-arcs has a negative reduced cost.
-__global__ void k_fresh_prices(int n, const unsigned char* __restrict__ fresh, const int* __restrict__ perm,
-                               DG g) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
+__global__ void k_fresh_prices(int ncap, const unsigned char* __restrict__ fresh, const int* __restrict__ perm, DG g) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
         if (!fresh[v]) continue;
         const int x = perm[v];
         long long best = -INF64;
@@ -1487,36 +1577,30 @@ __global__ void k_max_viol(DG g, long long m2) {
     if (lane_id() == 0 && mx > 0) __hip_atomic_fetch_max(&g.ctl->gu_L, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void k_save_prices(int n, const int* __restrict__ perm, const long long* __restrict__ p0,
-                              long long* __restrict__ pslot) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK)
-        pslot[v] = p0[perm[v]];
-}
-
 // ================================================ task → PU mapping ===
 // Path decomposition of the solved flow on device (replaces parseFlowToMapping,
 // placement/solver.go:183-269). Flow units are numbered per node: the units
-// leaving x are numbered along x's forward arcs in CSR order (out prefix), the
+// leaving x are numbered along x's forward arcs in segment order (out prefix), the
 // units entering y along y's reverse arcs (in prefix); unit k entering y leaves
 // on y's k-th outgoing unit. A task's single unit is followed until it reaches a
 // node without outflow (the sink); the last PU on the way is its placement.
-__global__ void k_unit_vals(long long m2, const int* __restrict__ vals, const long long* __restrict__ flows,
+__global__ void k_unit_vals(long long m2cap, const int* __restrict__ ent, const long long* __restrict__ flows,
                             long long* __restrict__ outv, long long* __restrict__ inv) {
-    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
-        const int v = vals[p];
-        const long long f = flows[v >> 1];
-        outv[p] = (v & 1) ? 0 : f;
-        inv[p] = (v & 1) ? f : 0;
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2cap; p += (long long)gridDim.x * BLK) {
+        const int e = ent[p];
+        const long long f = e >= 0 ? flows[e >> 1] : 0;
+        outv[p] = (e >= 0 && !(e & 1)) ? f : 0;
+        inv[p] = (e >= 0 && (e & 1)) ? f : 0;
     }
 }
 
-__global__ void k_node_meta(int n, const int* __restrict__ perm, const unsigned char* __restrict__ type,
-                            int* __restrict__ iperm, unsigned char* __restrict__ itype, int* __restrict__ is_task) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
-        const int x = perm[v];
-        iperm[x] = (int)v;
-        itype[x] = type[v];
-        is_task[v] = type[v] == KS_NODE_TASK ? 1 : 0;
+__global__ void k_node_meta(int ncap, const int* __restrict__ perm, const unsigned char* __restrict__ type,
+                            const unsigned char* __restrict__ alive, unsigned char* __restrict__ itype,
+                            int* __restrict__ is_task) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
+        const unsigned char t = alive[v] ? type[v] : 0;
+        itype[perm[v]] = t;
+        is_task[v] = t == KS_NODE_TASK ? 1 : 0;
     }
 }
 
@@ -1532,15 +1616,15 @@ __device__ __forceinline__ int find_unit(const long long* __restrict__ scan, con
     return lo;
 }
 
-__global__ void k_task_paths(int n, int nn, const int* __restrict__ perm, const int* __restrict__ first,
+__global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, const int* __restrict__ first,
                              const int* __restrict__ head, const int* __restrict__ rev,
                              const long long* __restrict__ outv, const long long* __restrict__ outs,
                              const long long* __restrict__ inv, const long long* __restrict__ ins,
                              const int* __restrict__ iperm, const unsigned char* __restrict__ itype,
-                             const int* __restrict__ rank, const unsigned char* __restrict__ type,
+                             const int* __restrict__ rank, const int* __restrict__ is_task,
                              unsigned long long* __restrict__ out) {
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < n; v += (long long)gridDim.x * BLK) {
-        if (type[v] != KS_NODE_TASK) continue;
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
+        if (!is_task[v]) continue;
         int x = perm[v];
         long long k = 0;   // unit index among x's outgoing units
         int last_pu = -1;
@@ -1559,6 +1643,22 @@ __global__ void k_task_paths(int n, int nn, const int* __restrict__ perm, const 
             x = y;
         }
         out[rank[v]] = last_pu >= 0 ? (unsigned long long)iperm[last_pu] + 1 : 0ULL;
+    }
+}
+
+// positive-flow arcs of the last solve as "f" records (ks_flow), slot order
+struct FlowPositive {
+    const unsigned char* alive;
+    const long long* flows;
+    __host__ __device__ bool operator()(const int& s) const { return alive[s] && flows[s] > 0; }
+};
+
+__global__ void k_flow_records(int cnt, const int* __restrict__ sel, const int* __restrict__ src,
+                               const int* __restrict__ dst, const long long* __restrict__ flows,
+                               ks_flow* __restrict__ out) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < cnt; i += (long long)gridDim.x * BLK) {
+        const int s = sel[i];
+        out[i] = ks_flow{(uint64_t)src[s] + 1, (uint64_t)dst[s] + 1, flows[s]};
     }
 }
 
@@ -1583,6 +1683,22 @@ struct DBuf {
         if (e == hipSuccess) n = want;
         return e;
     }
+    // grow to ≥ k elements keeping the first `keep` ones; new tail bytes = fill
+    hipError_t grow(size_t k, size_t keep, int fill, hipStream_t st) {
+        if (k <= n && p) return hipSuccess;
+        const size_t want = std::max<size_t>(k, 1);
+        T* q = nullptr;
+        hipError_t e = hipMalloc(&q, want * sizeof(T));
+        if (e != hipSuccess) return e;
+        keep = std::min(keep, n);
+        if (keep && p) e = hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipMemsetAsync(q + keep, fill, (want - keep) * sizeof(T), st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (p) (void)hipFree(p);
+        p = q;
+        n = want;
+        return e;
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -1599,22 +1715,38 @@ struct EngineImpl {
     hipEvent_t ev[8] = {};
     hipEvent_t kev[4] = {};   // per-cycle kernel-batch timing: BF rounds, sweeps
 
-    // input (compacted) graph, original ids
-    int64_t n = 0, m = 0;
-    int64_t maxc = 0;
-    DBuf<int> a_src, a_dst;
-    DBuf<long long> a_low, a_cap, a_cost, supply;
-    DBuf<unsigned char> a_type;   // DIMACS node type per slot (task/PU for the mapping)
-
-    // residual CSR and node state, internal ids
-    DBuf<unsigned> keys_in, keys_out;
-    DBuf<int> vals_in, vals_out, pos_of;
-    DBuf<unsigned char> sort_tmp;
-    DBuf<int> first, head, rev, fwd, perm;
+    // ---- node store (by slot = id − 1)
+    int64_t nstore = 0;       // allocated slots
+    int64_t nslots = 0;       // slots in use (max id)
+    DBuf<long long> n_supply;
+    DBuf<unsigned char> n_type, n_alive, n_fresh;
+    DBuf<int> n_lastrm;
+    // ---- arc table (by slot) and its hash index
+    int64_t acap = 0;
+    DBuf<int> a_src, a_dst, fwd, free_stack;
+    DBuf<long long> a_low, a_cap, a_cost;
+    DBuf<unsigned char> a_alive;
+    int64_t hcap = 0;
+    DBuf<unsigned long long> hkey;
+    DBuf<int> hval, hlast;
+    DBuf<StoreCtl> sctl;
+    StoreCtl* h_sctl = nullptr;   // pinned mirror
+    DBuf<ks_delta> d_recs;
+    DBuf<NodeEdit> d_edits;
+    DBuf<int> rec_ent;
+    // ---- residual CSR built from the table (internal ids)
+    bool csr_valid = false;   // CSR matches the table (deltas applied in place)
+    bool incremental = false; // deltas seen since the load: rebuild with slack
+    int64_t ncap = 0;         // node slots covered by the build
+    long long mult = 1;       // cost multiplier (ncap + 1)
+    int64_t m2cap = 0;        // residual positions (Σ segment capacities)
+    DBuf<int> first, head, rev, ent, used, perm, iperm;
     DBuf<long long> rcap, ucap, scost, excess, p0, p1, dist;
-    DBuf<unsigned char> cls;
+    DBuf<unsigned> keys_in, keys_out;
+    DBuf<int> vals_in, vals_out, pos_of, deg, capv, capi, rs;
+    DBuf<unsigned char> sort_tmp, cls;
     DBuf<int> nsel;
-    DBuf<int> cls_list[NGC + 1];   // original ids of each degree class; [NGC] = heavy hubs
+    DBuf<int> cls_list[NGC + 1];   // node slots of each degree class; [NGC] = heavy hubs
     DBuf<unsigned char> sel_tmp;
     DBuf<HItem> hitems;
     DBuf<CItem> citems;
@@ -1623,50 +1755,47 @@ struct EngineImpl {
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
-    DBuf<unsigned> trace;
-    DBuf<unsigned long long> stamps;
     DBuf<Ctl> ctl;
-    Ctl* h_ctl = nullptr;       // pinned host mirror
-    long long* h_scr = nullptr; // pinned scratch: [0] eps
+    Ctl* h_ctl = nullptr;        // pinned host mirror
+    long long* h_scr = nullptr;  // pinned scratch: [0] eps, [1] max |cost|
     int ncls[NGC + 1] = {0};
     int nheavy = 0, nhitems = 0, ncitems = 0;
-    int hub_base = 0, nn = 0;   // grouped node ids [0, hub_base), hubs after: nn ids
+    int hub_base = 0, nn = 0;    // grouped node ids [0, hub_base), hubs after: nn ids
     int obeg[NGC + 1] = {0}, oend[NGC] = {0}, wbeg[NGC + 1] = {0};
-    bool solved = false;
-    // warm start: the last successful solve's flows (input order) and prices (by slot)
-    DBuf<int> a_prev;              // per input arc: index in the previous upload, −1 = new
-    DBuf<unsigned char> a_fresh;   // per node slot: created since the previous solve
-    DBuf<long long> prev_flows, p_slot;
-    bool has_prev = false, fresh_valid = false;
-    int map_state = 0;             // 0 no mapping, 1 same arcs as the last solve, 2 a_prev
-    int64_t n_prev = 0;
-    long long mult_prev = 1;
-    // device mapping extraction scratch
-    DBuf<long long> map_outv, map_inv, map_outs, map_ins;
-    DBuf<int> map_iperm, map_rank;
-    DBuf<unsigned char> map_itype, map_tmp;
-    DBuf<uint64_t> map_scratch;   // device vector behind ks_get_task_mapping
+    // ---- solution
+    bool solved = false;         // flows/prices of the current graph are optimal
+    bool has_prev = false;       // a solution exists in place (warm start possible)
     int64_t n_tasks = 0;
+    DBuf<long long> saved_flows, p_slot;
+    DBuf<long long> map_outv, map_inv, map_outs, map_ins;
+    DBuf<int> map_rank, map_is_task, flow_sel, flow_cnt;
+    DBuf<unsigned char> map_itype, map_tmp;
+    DBuf<uint64_t> map_scratch;  // device vector behind ks_get_task_mapping
+    DBuf<ks_flow> flow_recs;
 
     ~EngineImpl() {
         if (stream) {
             (void)hipSetDevice(device);
             (void)hipStreamSynchronize(stream);
         }
-        a_src.release(); a_dst.release(); a_low.release(); a_cap.release(); a_cost.release(); supply.release();
-        keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release();
-        sort_tmp.release(); first.release(); head.release(); rev.release(); fwd.release(); perm.release();
-        rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release();
-        dist.release(); cls.release(); nsel.release();
+        n_supply.release(); n_type.release(); n_alive.release(); n_fresh.release(); n_lastrm.release();
+        a_src.release(); a_dst.release(); fwd.release(); free_stack.release(); a_low.release(); a_cap.release();
+        a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
+        d_recs.release(); d_edits.release(); rec_ent.release();
+        first.release(); head.release(); rev.release(); ent.release(); used.release(); perm.release(); iperm.release();
+        rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release(); dist.release();
+        keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
+        capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
-        sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release();
-        q_arrive.release(); q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release(); flags.release(); hubflags.release();
-        ctr.release(); trace.release(); stamps.release(); ctl.release();
-        a_prev.release(); a_fresh.release(); prev_flows.release(); p_slot.release();
-        a_type.release(); map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release();
-        map_iperm.release(); map_itype.release(); map_rank.release(); map_tmp.release(); map_scratch.release();
+        sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
+        q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
+        flags.release(); hubflags.release(); ctr.release(); ctl.release(); saved_flows.release(); p_slot.release();
+        map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
+        map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
+        map_scratch.release(); flow_recs.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (h_scr) (void)hipHostFree(h_scr);
+        if (h_sctl) (void)hipHostFree(h_sctl);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& e : kev)
@@ -1674,10 +1803,48 @@ struct EngineImpl {
         if (stream) (void)hipStreamDestroy(stream);
     }
 
+    StoreDev sd() const {
+        StoreDev d{};
+        d.ncap = (int)ncap;
+        d.n_supply = n_supply.p;
+        d.n_type = n_type.p;
+        d.n_alive = n_alive.p;
+        d.n_fresh = n_fresh.p;
+        d.n_lastrm = n_lastrm.p;
+        d.perm = perm.p;
+        d.acap = (int)acap;
+        d.a_src = a_src.p;
+        d.a_dst = a_dst.p;
+        d.a_low = a_low.p;
+        d.a_cap = a_cap.p;
+        d.a_cost = a_cost.p;
+        d.a_alive = a_alive.p;
+        d.fwd = fwd.p;
+        d.free_stack = free_stack.p;
+        d.hmask = (int)(hcap - 1);
+        d.hkey = hkey.p;
+        d.hval = hval.p;
+        d.hlast = hlast.p;
+        d.nn = nn;
+        d.first = first.p;
+        d.used = used.p;
+        d.head = head.p;
+        d.rev = rev.p;
+        d.ent = ent.p;
+        d.rcap = rcap.p;
+        d.ucap = ucap.p;
+        d.scost = scost.p;
+        d.excess = excess.p;
+        d.mult = mult;
+        d.csr_valid = csr_valid ? 1 : 0;
+        d.ctl = sctl.p;
+        return d;
+    }
+
     DG dg() const {
         DG g{};
         g.n = nn;
-        g.m = (int)m;
+        g.m = 0;
         g.hub_base = hub_base;
         g.first = first.p;
         g.head = head.p;
@@ -1715,14 +1882,12 @@ struct EngineImpl {
         }
         g.ctl = ctl.p;
         g.ctr = ctr.p;
-        g.trace = trace.n > 1 ? trace.p : nullptr;
-        g.stamps = stamps.n > 1 ? stamps.p : nullptr;
-        g.stamp_sweep = -1;
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
     int dense_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
     int sparse_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB)); }
+    int hi() const { return h_sctl->hi; }
 };
 
 #define KS_CHECK(expr)                                                   \
@@ -1754,248 +1919,211 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
+    KS_CHECK(s.sctl.ensure(1));
+    KS_CHECK(hipMemset(s.sctl.p, 0, sizeof(StoreCtl)));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
     KS_CHECK(hipHostMalloc(&s.h_scr, 4 * sizeof(long long)));
+    KS_CHECK(hipHostMalloc(&s.h_sctl, sizeof(StoreCtl)));
+    std::memset(s.h_sctl, 0, sizeof(StoreCtl));
     return KS_OK;
 }
 
-int Engine::upload(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int64_t* low,
-                   const int64_t* cap, const int64_t* cost, const int64_t* supply, const uint8_t* type,
-                   const int32_t* prev_idx, const uint8_t* fresh, std::string& err) {
-    EngineImpl& s = *p_;
-    KS_CHECK(hipSetDevice(s.device));
-    if (n < 0 || m < 0 || n > (1LL << 28) || m > (1LL << 29)) {
-        err = "graph too large for 32-bit CSR indices";
-        return KS_E_RANGE;
-    }
-    s.n = n;
-    s.m = m;
-    s.solved = false;
-    s.maxc = 0;
-    for (int64_t i = 0; i < m; ++i) s.maxc = std::max<int64_t>(s.maxc, cost[i] < 0 ? -cost[i] : cost[i]);
-    KS_CHECK(s.a_src.ensure(m));
-    KS_CHECK(s.a_dst.ensure(m));
-    KS_CHECK(s.a_low.ensure(m));
-    KS_CHECK(s.a_cap.ensure(m));
-    KS_CHECK(s.a_cost.ensure(m));
-    KS_CHECK(s.supply.ensure(n));
-    if (m) {
-        KS_CHECK(hipMemcpyAsync(s.a_src.p, src, m * sizeof(int), hipMemcpyHostToDevice, s.stream));
-        KS_CHECK(hipMemcpyAsync(s.a_dst.p, dst, m * sizeof(int), hipMemcpyHostToDevice, s.stream));
-        KS_CHECK(hipMemcpyAsync(s.a_low.p, low, m * sizeof(long long), hipMemcpyHostToDevice, s.stream));
-        KS_CHECK(hipMemcpyAsync(s.a_cap.p, cap, m * sizeof(long long), hipMemcpyHostToDevice, s.stream));
-        KS_CHECK(hipMemcpyAsync(s.a_cost.p, cost, m * sizeof(long long), hipMemcpyHostToDevice, s.stream));
-    }
-    if (n) KS_CHECK(hipMemcpyAsync(s.supply.p, supply, n * sizeof(long long), hipMemcpyHostToDevice, s.stream));
-    KS_CHECK(s.a_type.ensure(n));
-    s.n_tasks = 0;
-    for (int64_t v = 0; v < n; ++v) s.n_tasks += type[v] == KS_NODE_TASK;
-    if (n) KS_CHECK(hipMemcpyAsync(s.a_type.p, type, n, hipMemcpyHostToDevice, s.stream));
-    s.map_state = 0;
-    s.fresh_valid = false;
-    if (prev_idx && s.has_prev) {
-        KS_CHECK(s.a_prev.ensure(m));
-        if (m) KS_CHECK(hipMemcpyAsync(s.a_prev.p, prev_idx, m * sizeof(int), hipMemcpyHostToDevice, s.stream));
-        s.map_state = 2;
-        if (fresh && n) {
-            KS_CHECK(s.a_fresh.ensure(n));
-            KS_CHECK(hipMemcpyAsync(s.a_fresh.p, fresh, n, hipMemcpyHostToDevice, s.stream));
-            s.fresh_valid = true;
-        }
-    }
+// ------------------------------------------------------------------ store ---
+static int read_sctl(EngineImpl& s, std::string& err) {
+    KS_CHECK(hipMemcpyAsync(s.h_sctl, s.sctl.p, sizeof(StoreCtl), hipMemcpyDeviceToHost, s.stream));
     KS_CHECK(hipStreamSynchronize(s.stream));
     return KS_OK;
 }
 
-int Engine::task_pu(uint64_t* dev_out, size_t cap, size_t* count, std::string& err) {
-    EngineImpl& s = *p_;
-    if (!s.solved) {
-        err = "no successful solve";
-        return KS_E_INVALID;
-    }
-    KS_CHECK(hipSetDevice(s.device));
+// Node store covers slots [0, need).
+static int ensure_nodes(EngineImpl& s, int64_t need, std::string& err) {
+    if (need <= s.nstore) return KS_OK;
+    const int64_t cap = std::max<int64_t>(need + need / 8 + 64, 1024);
     hipStream_t st = s.stream;
-    *count = (size_t)s.n_tasks;
-    if (!dev_out || cap < (size_t)s.n_tasks || s.n_tasks == 0) {
-        if (dev_out && cap < (size_t)s.n_tasks) {
-            err = "output buffer smaller than the task count";
-            return KS_E_INVALID;
-        }
-        return KS_OK;
-    }
-    const int64_t n = s.n, m2 = 2 * s.m;
-    const int nn = s.nn;
-    KS_CHECK(s.map_outv.ensure(m2));
-    KS_CHECK(s.map_inv.ensure(m2));
-    KS_CHECK(s.map_outs.ensure(m2));
-    KS_CHECK(s.map_ins.ensure(m2));
-    KS_CHECK(s.map_iperm.ensure(nn));
-    KS_CHECK(s.map_itype.ensure(nn));
-    KS_CHECK(s.map_rank.ensure(2 * n));
-    KS_CHECK(hipMemsetAsync(s.map_itype.p, 0, nn, st));
-    if (m2)
-        hipLaunchKernelGGL(k_unit_vals, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, (const int*)s.vals_out.p,
-                           (const long long*)s.flows.p, s.map_outv.p, s.map_inv.p);
-    hipLaunchKernelGGL(k_node_meta, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const int*)s.perm.p,
-                       (const unsigned char*)s.a_type.p, s.map_iperm.p, s.map_itype.p, s.map_rank.p + n);
-    size_t t1 = 0, t2 = 0;
-    if (m2) KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.map_outv.p, s.map_outs.p, (int)m2, st));
-    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, s.map_rank.p + n, s.map_rank.p, (int)n, st));
-    KS_CHECK(s.map_tmp.ensure(std::max(t1, t2)));
-    size_t tt = s.map_tmp.n;
-    if (m2) {
-        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_outv.p, s.map_outs.p, (int)m2, st));
-        tt = s.map_tmp.n;
-        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_inv.p, s.map_ins.p, (int)m2, st));
-    }
-    tt = s.map_tmp.n;
-    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_rank.p + n, s.map_rank.p, (int)n, st));
-    hipLaunchKernelGGL(k_task_paths, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, nn, (const int*)s.perm.p,
-                       (const int*)s.first.p, (const int*)s.head.p, (const int*)s.rev.p,
-                       (const long long*)s.map_outv.p, (const long long*)s.map_outs.p,
-                       (const long long*)s.map_inv.p, (const long long*)s.map_ins.p,
-                       (const int*)s.map_iperm.p, (const unsigned char*)s.map_itype.p, (const int*)s.map_rank.p,
-                       (const unsigned char*)s.a_type.p, (unsigned long long*)dev_out);
-    KS_CHECK(hipGetLastError());
-    KS_CHECK(hipStreamSynchronize(st));
+    KS_CHECK(s.n_supply.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_type.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_alive.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_fresh.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_lastrm.grow(cap, s.nstore, 0xff, st));
+    s.nstore = cap;
     return KS_OK;
 }
 
-int Engine::download(void* host_dst, const void* dev_src, size_t bytes, std::string& err) {
-    EngineImpl& s = *p_;
-    KS_CHECK(hipSetDevice(s.device));
-    if (bytes) {
-        KS_CHECK(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, s.stream));
-        KS_CHECK(hipStreamSynchronize(s.stream));
-    }
-    return KS_OK;
-}
-
-int Engine::scratch(uint64_t** dev, size_t n, std::string& err) {
-    EngineImpl& s = *p_;
-    KS_CHECK(hipSetDevice(s.device));
-    KS_CHECK(s.map_scratch.ensure(std::max<size_t>(1, n)));
-    *dev = s.map_scratch.p;
-    return KS_OK;
-}
-
-
-// "index:path" → index, path
-static bool g_trace_ok(const char* spec, int& idx, std::string& path) {
-    const char* c = std::strchr(spec, ':');
-    if (!c) return false;
-    idx = std::atoi(spec);
-    path = c + 1;
-    return true;
-}
-
-static double ev_ms(hipEvent_t a, hipEvent_t b) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
-    return ms;
-}
-
-int Engine::solve(ks_result& res, bool warm, std::string& err) {
-    EngineImpl& s = *p_;
-    KS_CHECK(hipSetDevice(s.device));
-    const auto t_host0 = std::chrono::steady_clock::now();
-    auto wall_s = [&]() {
-        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count();
-    };
-    hipStream_t st = s.stream;
-    const int64_t n = s.n, m = s.m, m2 = 2 * m;
-    const bool use_warm = warm && s.has_prev && s.map_state != 0;
-    s.solved = false;
-    s.has_prev = false;
-    if (use_warm) {   // the last solution becomes the warm-start input
-        std::swap(s.flows.p, s.prev_flows.p);
-        std::swap(s.flows.n, s.prev_flows.n);
-    }
-    res.warm_started = use_warm ? 1 : 0;
-    res.n_nodes = n;
-    res.n_arcs = m;
-    if (n == 0) {
-        res.total_cost = 0;
-        res.flow_value = 0;   // no arcs: nothing flows
-        s.solved = true;
-        return KS_OK;
-    }
-    const long long mult = n + 1;
-    if (s.maxc > 0 && (double)s.maxc * (double)mult * 8.0 * (double)(n + 1) > 4.0e18) {
-        err = "cost range too large for int64 scaled prices";
+// Arc table holds slots [0, need).
+static int ensure_arcs(EngineImpl& s, int64_t need, std::string& err) {
+    if (need <= s.acap) return KS_OK;
+    if (need >= (1LL << 30)) {
+        err = "arc table beyond 2^30 slots";
         return KS_E_RANGE;
     }
+    const int64_t cap = std::max<int64_t>(need + need / 4 + 64, 4096);
+    hipStream_t st = s.stream;
+    const int64_t keep = s.acap;
+    KS_CHECK(s.a_src.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_dst.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_low.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_cap.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_cost.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_alive.grow(cap, keep, 0, st));
+    KS_CHECK(s.fwd.grow(cap, keep, 0xff, st));
+    KS_CHECK(s.free_stack.grow(cap, keep, 0, st));
+    KS_CHECK(s.flows.grow(cap, keep, 0, st));
+    s.acap = cap;
+    return KS_OK;
+}
 
-    // ------------------------------------------------------------ build ---
-    KS_CHECK(hipEventRecord(s.ev[0], st));
-    KS_CHECK(s.keys_in.ensure(m2));
-    KS_CHECK(s.keys_out.ensure(m2));
-    KS_CHECK(s.vals_in.ensure(m2));
-    KS_CHECK(s.vals_out.ensure(m2));
-    KS_CHECK(s.pos_of.ensure(m2));
-    KS_CHECK(s.head.ensure(m2));
-    KS_CHECK(s.rev.ensure(m2));
-    KS_CHECK(s.fwd.ensure(m));
-    KS_CHECK(s.rcap.ensure(m2));
-    KS_CHECK(s.ucap.ensure(m2));
-    KS_CHECK(s.scost.ensure(m2));
-    KS_CHECK(s.perm.ensure(n));
-    KS_CHECK(s.cls.ensure(n));
-    for (auto& b : s.cls_list) KS_CHECK(b.ensure(n));
+// Hash index with room for `extra` more keys at load ≤ 1/2 (tombstones count).
+static int ensure_hash(EngineImpl& s, int64_t extra, std::string& err) {
+    const int64_t live = s.h_sctl->live, tombs = s.h_sctl->tombs;
+    if (s.hcap && 2 * (live + tombs + extra) <= s.hcap) return KS_OK;
+    int64_t cap = s.hcap ? s.hcap : 1024;
+    while (cap < 4 * (live + extra) + 1024) cap <<= 1;
+    if (cap > (1LL << 31)) {
+        err = "hash index beyond 2^31 entries";
+        return KS_E_RANGE;
+    }
+    KS_CHECK(s.hkey.ensure(cap));
+    KS_CHECK(s.hval.ensure(cap));
+    KS_CHECK(s.hlast.ensure(cap));
+    s.hcap = cap;
+    KS_CHECK(store_rehash(s.sd(), s.stream));
+    return read_sctl(s, err);
+}
+
+static int run_apply(EngineImpl& s, const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t k,
+                     std::string& err) {
+    hipStream_t st = s.stream;
+    size_t narc = 0;
+    for (size_t i = 0; i < k; ++i) narc += recs[i].kind == KS_ADD_ARC || recs[i].kind == KS_UPDATE_ARC;
+    int rc = ensure_arcs(s, (int64_t)s.hi() + (int64_t)narc, err);
+    if (rc == KS_OK) rc = ensure_hash(s, (int64_t)narc, err);
+    if (rc) return rc;
+    KS_CHECK(s.d_recs.ensure(std::max<size_t>(k, 1)));
+    KS_CHECK(s.rec_ent.ensure(std::max<size_t>(k, 1)));
+    KS_CHECK(s.d_edits.ensure(std::max<size_t>(ne, 1)));
+    if (k) KS_CHECK(hipMemcpyAsync(s.d_recs.p, recs, k * sizeof(ks_delta), hipMemcpyHostToDevice, st));
+    if (ne) KS_CHECK(hipMemcpyAsync(s.d_edits.p, edits, ne * sizeof(NodeEdit), hipMemcpyHostToDevice, st));
+    KS_CHECK(store_apply(s.sd(), s.d_recs.p, (int)k, s.rec_ent.p, s.d_edits.p, (int)ne, st));
+    rc = read_sctl(s, err);
+    if (rc) return rc;
+    if (s.h_sctl->overflow & 12) {
+        err = "store index or table exhausted";
+        return KS_E_DEVICE;
+    }
+    if (s.h_sctl->overflow) {   // a full segment or a node beyond the build: rebuild from the table
+        s.csr_valid = false;
+        KS_CHECK(hipMemsetAsync(&s.sctl.p->overflow, 0, sizeof(int), st));
+        s.h_sctl->overflow = 0;
+    }
+    if (k || ne) s.solved = false;
+    return KS_OK;
+}
+
+int Engine::load(int64_t nslots, const int64_t* supply, const uint8_t* type, const uint8_t* alive, const ks_arc* arcs,
+                 size_t m, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    if (nslots >= (1LL << 30) || m >= (1ULL << 29)) {
+        err = "graph too large for 32-bit CSR indices";
+        return KS_E_RANGE;
+    }
+    int rc = ensure_nodes(s, std::max<int64_t>(nslots, 1), err);
+    if (rc) return rc;
+    s.nslots = nslots;
+    // empty store
+    KS_CHECK(hipMemsetAsync(s.n_alive.p, 0, s.nstore, st));
+    KS_CHECK(hipMemsetAsync(s.n_supply.p, 0, s.nstore * sizeof(long long), st));
+    KS_CHECK(hipMemsetAsync(s.n_type.p, 0, s.nstore, st));
+    KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
+    if (nslots) {
+        KS_CHECK(hipMemcpyAsync(s.n_supply.p, supply, nslots * sizeof(long long), hipMemcpyHostToDevice, st));
+        KS_CHECK(hipMemcpyAsync(s.n_type.p, type, nslots, hipMemcpyHostToDevice, st));
+        KS_CHECK(hipMemcpyAsync(s.n_alive.p, alive, nslots, hipMemcpyHostToDevice, st));
+    }
+    if (s.acap) {
+        KS_CHECK(hipMemsetAsync(s.a_alive.p, 0, s.acap, st));
+        KS_CHECK(hipMemsetAsync(s.fwd.p, 0xff, s.acap * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.a_low.p, 0, s.acap * sizeof(long long), st));
+    }
+    KS_CHECK(hipMemsetAsync(s.sctl.p, 0, sizeof(StoreCtl), st));
+    std::memset(s.h_sctl, 0, sizeof(StoreCtl));
+    s.csr_valid = false;
+    s.incremental = false;
+    s.solved = false;
+    s.has_prev = false;
+    rc = ensure_arcs(s, (int64_t)m, err);
+    if (rc) return rc;
+    if (s.hcap) {   // clear the index (keeps its size)
+        KS_CHECK(hipMemsetAsync(s.hkey.p, 0, s.hcap * sizeof(unsigned long long), st));
+        KS_CHECK(hipMemsetAsync(s.hval.p, 0xff, s.hcap * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.hlast.p, 0xff, s.hcap * sizeof(int), st));
+    }
+    // the arcs enter as ADD_ARC records of one stream (duplicates: the last wins)
+    std::vector<ks_delta> recs(m);
+    for (size_t i = 0; i < m; ++i) {
+        ks_delta& d = recs[i];
+        std::memset(&d, 0, sizeof(d));
+        d.kind = KS_ADD_ARC;
+        d.type = arcs[i].type;
+        d.src = arcs[i].src;
+        d.dst = arcs[i].dst;
+        d.low = arcs[i].low;
+        d.cap = arcs[i].cap;
+        d.cost = arcs[i].cost;
+    }
+    return run_apply(s, nullptr, 0, recs.data(), m, err);
+}
+
+int Engine::apply(const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t k, int64_t nslots,
+                  std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    int rc = ensure_nodes(s, std::max<int64_t>(nslots, 1), err);
+    if (rc) return rc;
+    s.nslots = std::max(s.nslots, nslots);
+    s.incremental = true;
+    return run_apply(s, edits, ne, recs, k, err);
+}
+
+int64_t Engine::live_arcs() const { return p_->h_sctl ? p_->h_sctl->live : 0; }
+
+// ------------------------------------------------------------------ build ---
+static int build(EngineImpl& s, std::string& err) {
+    hipStream_t st = s.stream;
+    const int hi = s.hi();
+    const int64_t spare = s.incremental ? std::max<int64_t>(64, s.nslots / 16) : 0;
+    const int64_t ncap = s.nslots + spare;
+    int rc = ensure_nodes(s, ncap, err);
+    if (rc) return rc;
+    s.ncap = ncap;
+    s.mult = ncap + 1;
+    KS_CHECK(s.deg.ensure(std::max<int64_t>(ncap, 1)));
+    KS_CHECK(s.capv.ensure(std::max<int64_t>(ncap, 1)));
+    KS_CHECK(s.cls.ensure(std::max<int64_t>(ncap, 1)));
+    KS_CHECK(s.perm.ensure(std::max<int64_t>(ncap, 1)));
+    for (auto& b : s.cls_list) KS_CHECK(b.ensure(std::max<int64_t>(ncap, 1)));
     KS_CHECK(s.nsel.ensure(NGC + 1));
-    KS_CHECK(s.flows.ensure(m));
-    KS_CHECK(s.part.ensure(2 * 4096));   // per-block cost sums, then flow-value sums
-    KS_CHECK(s.first.ensure(n + 2 + 64 * NGC));
-    KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
-    KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
-    std::memset(s.h_ctl, 0, sizeof(Ctl));
-    const char* trace_path = std::getenv("KS_TRACE");
-    if (trace_path && *trace_path) {
-        KS_CHECK(s.trace.ensure(4 * kTraceMax));
-        KS_CHECK(hipMemsetAsync(s.trace.p, 0, 4 * kTraceMax * sizeof(unsigned), st));
-    } else {
-        s.trace.release();
-    }
-    struct PhaseRec {
-        long long eps;
-        uint64_t begin, end;
-        std::vector<uint64_t> gu_at;
-        int pr_rounds;   // price-refinement rounds; > 0 success, < 0 failed
-    };
-    std::vector<PhaseRec> ptrace;
-
-    int bits = 1;
-    while ((1LL << bits) <= n + 64 * NGC + 1) ++bits;
-    size_t sort_tmp = 0;
-    // 1. degrees in original ids (sorted endpoint keys) → degree classes
-    if (m) {
-        hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
-                           (const int*)nullptr, s.keys_in.p, (int*)nullptr);
-        KS_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_tmp, s.keys_in.p, s.keys_out.p, (int)m2, 0, bits,
-                                                   st));
-        size_t t2 = 0;
-        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, s.keys_in.p, s.keys_out.p, s.vals_in.p,
-                                                    s.vals_out.p, (int)m2, 0, bits, st));
-        sort_tmp = std::max(sort_tmp, t2);
-        KS_CHECK(s.sort_tmp.ensure(sort_tmp));
-        KS_CHECK(hipcub::DeviceRadixSort::SortKeys(s.sort_tmp.p, sort_tmp, s.keys_in.p, s.keys_out.p, (int)m2, 0,
-                                                   bits, st));
-    }
-    hipLaunchKernelGGL(k_first, dim3(grid_for(n + 1)), dim3(BLK), 0, st, (int)n, (long long)m2, s.keys_out.p,
-                       s.first.p);
-    hipLaunchKernelGGL(k_classify, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const int*)s.first.p, s.cls.p);
+    KS_CHECK(s.part.ensure(2 * 4096));
+    KS_CHECK(hipMemsetAsync(s.deg.p, 0, ncap * sizeof(int), st));
+    // 1. degrees → segment capacities → classes
+    if (hi)
+        hipLaunchKernelGGL(k_degree, dim3(grid_for(hi)), dim3(BLK), 0, st, hi, (const unsigned char*)s.a_alive.p,
+                           (const int*)s.a_src.p, (const int*)s.a_dst.p, s.deg.p);
+    hipLaunchKernelGGL(k_capacity, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, (int)s.nstore,
+                       (const int*)s.deg.p, (const unsigned char*)s.n_alive.p, s.incremental ? 1 : 0, s.capv.p, s.cls.p);
     {
         hipcub::CountingInputIterator<int> it(0);
         size_t tmp = 0, t2 = 0;
         for (unsigned char c = 0; c <= NGC; ++c) {
-            KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)n,
+            KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
                                               ClassIs{s.cls.p, c}, st));
             tmp = std::max(tmp, t2);
         }
         KS_CHECK(s.sel_tmp.ensure(tmp));
         for (unsigned char c = 0; c <= NGC; ++c) {
             t2 = tmp;
-            KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)n,
+            KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
                                               ClassIs{s.cls.p, c}, st));
         }
     }
@@ -2023,33 +2151,76 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (s.ncls[c])
             hipLaunchKernelGGL(k_make_perm, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c],
                                c < NGC ? s.obeg[c] : s.hub_base, (const int*)s.cls_list[c].p, s.perm.p);
-    KS_CHECK(s.excess.ensure(nn));
-    KS_CHECK(s.p0.ensure(nn));
-    KS_CHECK(s.p1.ensure(nn));
-    KS_CHECK(s.dist.ensure(nn));
+    KS_CHECK(s.capi.ensure(nn + 1));
+    KS_CHECK(s.iperm.ensure(nn + 1));
     KS_CHECK(s.first.ensure(nn + 1));
-    // 3. residual CSR over internal ids
-    if (m) {
-        hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
-                           (const int*)s.perm.p, s.keys_in.p, s.vals_in.p);
-        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(s.sort_tmp.p, sort_tmp, s.keys_in.p, s.keys_out.p, s.vals_in.p,
-                                                    s.vals_out.p, (int)m2, 0, bits, st));
-        hipLaunchKernelGGL(k_scatter_pos, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, s.vals_out.p,
-                           s.pos_of.p);
-        hipLaunchKernelGGL(k_fill, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, mult, s.vals_out.p,
-                           s.pos_of.p, s.a_src.p, s.a_dst.p, (const int*)s.perm.p, s.a_low.p, s.a_cap.p, s.a_cost.p,
-                           s.head.p, s.rev.p, s.rcap.p, s.ucap.p, s.scost.p, s.fwd.p);
+    KS_CHECK(s.used.ensure(std::max(nn, 1)));
+    KS_CHECK(s.rs.ensure(nn + 1));
+    KS_CHECK(hipMemsetAsync(s.capi.p, 0, (nn + 1) * sizeof(int), st));
+    KS_CHECK(hipMemsetAsync(s.iperm.p, 0xff, (nn + 1) * sizeof(int), st));
+    hipLaunchKernelGGL(k_capi, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, (const int*)s.perm.p,
+                       (const int*)s.capv.p, s.capi.p, s.iperm.p);
+    {   // first = exclusive scan of the capacities (nn + 1 entries: first[nn] = Σ)
+        size_t t = 0;
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t, s.capi.p, s.first.p, nn + 1, st));
+        KS_CHECK(s.sort_tmp.ensure(std::max<size_t>(t, s.sort_tmp.n)));
+        t = s.sort_tmp.n;
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.sort_tmp.p, t, s.capi.p, s.first.p, nn + 1, st));
     }
-    hipLaunchKernelGGL(k_first, dim3(grid_for(nn + 1)), dim3(BLK), 0, st, nn, (long long)m2, s.keys_out.p,
-                       s.first.p);
-    hipLaunchKernelGGL(k_node_init, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, s.excess.p, s.p0.p, s.p1.p);
-    hipLaunchKernelGGL(k_supply, dim3(grid_for(n)), dim3(BLK), 0, st, (int)n, (const long long*)s.supply.p,
-                       (const int*)s.perm.p, s.excess.p);
-    if (m)
-        hipLaunchKernelGGL(k_lower_bounds, dim3(grid_for(m)), dim3(BLK), 0, st, (int)m, s.a_src.p, s.a_dst.p,
-                           (const int*)s.perm.p, s.a_low.p, s.excess.p);
+    int m2c = 0;
+    KS_CHECK(hipMemcpyAsync(&m2c, s.first.p + nn, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    s.m2cap = m2c;
+    const int64_t m2cap = std::max<int64_t>(m2c, 1);
+    KS_CHECK(s.head.ensure(m2cap));
+    KS_CHECK(s.rev.ensure(m2cap));
+    KS_CHECK(s.ent.ensure(m2cap));
+    KS_CHECK(s.rcap.ensure(m2cap));
+    KS_CHECK(s.ucap.ensure(m2cap));
+    KS_CHECK(s.scost.ensure(m2cap));
+    KS_CHECK(s.excess.ensure(std::max(nn, 1)));
+    KS_CHECK(s.p0.ensure(std::max(nn, 1)));
+    KS_CHECK(s.p1.ensure(std::max(nn, 1)));
+    KS_CHECK(s.dist.ensure(std::max(nn, 1)));
+    if (m2c)
+        hipLaunchKernelGGL(k_inert_all, dim3(grid_for(m2c)), dim3(BLK), 0, st, (long long)m2c, nn,
+                           (const int*)s.first.p, s.head.p, s.rev.p, s.ent.p, s.rcap.p, s.ucap.p, s.scost.p);
+    // 3. live arcs into their segments, ordered by tail (radix sort of 2·hi keys)
+    const int64_t m2 = 2 * (int64_t)hi;
+    if (s.acap) KS_CHECK(hipMemsetAsync(s.fwd.p, 0xff, s.acap * sizeof(int), st));
+    if (m2) {
+        KS_CHECK(s.keys_in.ensure(m2));
+        KS_CHECK(s.keys_out.ensure(m2));
+        KS_CHECK(s.vals_in.ensure(m2));
+        KS_CHECK(s.vals_out.ensure(m2));
+        KS_CHECK(s.pos_of.ensure(m2));
+        int bits = 1;
+        while ((1LL << bits) <= nn + 1) ++bits;
+        hipLaunchKernelGGL(k_pos_keys, dim3(grid_for(hi)), dim3(BLK), 0, st, hi, nn,
+                           (const unsigned char*)s.a_alive.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
+                           (const int*)s.perm.p, s.keys_in.p, s.vals_in.p);
+        size_t t = 0;
+        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t, s.keys_in.p, s.keys_out.p, s.vals_in.p,
+                                                    s.vals_out.p, (int)m2, 0, bits, st));
+        KS_CHECK(s.sort_tmp.ensure(std::max<size_t>(t, s.sort_tmp.n)));
+        t = s.sort_tmp.n;
+        KS_CHECK(hipcub::DeviceRadixSort::SortPairs(s.sort_tmp.p, t, s.keys_in.p, s.keys_out.p, s.vals_in.p,
+                                                    s.vals_out.p, (int)m2, 0, bits, st));
+        hipLaunchKernelGGL(k_first, dim3(grid_for(nn + 1)), dim3(BLK), 0, st, nn, (long long)m2,
+                           (const unsigned*)s.keys_out.p, s.rs.p);
+        hipLaunchKernelGGL(k_fill_csr, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, nn,
+                           (const unsigned*)s.keys_out.p, (const int*)s.vals_out.p, (const int*)s.rs.p,
+                           (const int*)s.first.p, (const int*)s.perm.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
+                           (const long long*)s.a_low.p, (const long long*)s.a_cap.p, (const long long*)s.a_cost.p,
+                           s.mult, s.head.p, s.rcap.p, s.ucap.p, s.scost.p, s.ent.p, s.fwd.p, s.pos_of.p);
+        hipLaunchKernelGGL(k_fill_rev, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, nn,
+                           (const unsigned*)s.keys_out.p, (const int*)s.vals_out.p, (const int*)s.pos_of.p, s.rev.p);
+        hipLaunchKernelGGL(k_used, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, (const int*)s.rs.p, s.used.p);
+    } else {
+        KS_CHECK(hipMemsetAsync(s.used.p, 0, std::max(nn, 1) * sizeof(int), st));
+    }
+    // 4. hub chunk table and the chunked class's 64-arc chunks (from the segments)
     {
-        // heavy hubs: chunk table (few hubs; built on host from their CSR ranges)
         std::vector<int> hf(s.nheavy + 1);
         if (s.nheavy) {
             KS_CHECK(hipMemcpyAsync(hf.data(), s.first.p + s.hub_base, (s.nheavy + 1) * sizeof(int),
@@ -2076,27 +2247,19 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_CHECK(hipMemcpyAsync(s.hitems.p, items.data(), items.size() * sizeof(HItem), hipMemcpyHostToDevice, st));
             KS_CHECK(hipMemcpyAsync(s.hnchunks.p, nch.data(), nch.size() * sizeof(int), hipMemcpyHostToDevice, st));
             KS_CHECK(hipMemsetAsync(s.inbox.p, 0, (size_t)s.nheavy * SHARDS * sizeof(long long), st));
-            KS_CHECK(hipStreamSynchronize(st));
         }
-    }
-    {
-        // chunked class: 64-arc chunk table (built on host from the class's CSR ranges)
         const int c0 = s.obeg[CCLS], cn = s.ncls[CCLS];
         std::vector<int> cf(cn + 1);
-        if (cn) {
-            KS_CHECK(hipMemcpyAsync(cf.data(), s.first.p + c0, (cn + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
-            KS_CHECK(hipStreamSynchronize(st));
-        }
+        if (cn) KS_CHECK(hipMemcpyAsync(cf.data(), s.first.p + c0, (cn + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipStreamSynchronize(st));
         std::vector<CItem> ci;
-        for (int k = 0; k < cn; ++k) {
+        for (int k = 0; k < cn; ++k)
             for (int b = cf[k]; b < cf[k + 1]; b += 64)
                 ci.push_back(CItem{c0 + k, b, std::min(b + 64, cf[k + 1]), b == cf[k] ? 1 : 0});
-        }
         s.ncitems = (int)ci.size();
         KS_CHECK(s.citems.ensure(std::max<size_t>(1, ci.size())));
         if (!ci.empty())
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
-        // claim slots: one per hub
         const int nq = std::max(1, s.nheavy);
         KS_CHECK(s.q_req.ensure(nq));
         KS_CHECK(s.q_taken.ensure(nq));
@@ -2111,18 +2274,229 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipMemsetAsync(s.q_arrive.p, 0, nq * sizeof(int), st));
         KS_CHECK(hipStreamSynchronize(st));
     }
+    s.csr_valid = true;
+    return KS_OK;
+}
+
+// zero flow, supplies with the lower-bound transform, zero prices
+static int cold_reset(EngineImpl& s, std::string& err) {
+    hipStream_t st = s.stream;
+    const int hi = s.hi();
+    if (s.m2cap)
+        hipLaunchKernelGGL(k_reset_pos, dim3(grid_for(s.m2cap)), dim3(BLK), 0, st, (long long)s.m2cap,
+                           (const int*)s.ent.p, (const long long*)s.ucap.p, s.rcap.p);
+    hipLaunchKernelGGL(k_reset_nodes, dim3(grid_for(s.nn)), dim3(BLK), 0, st, s.nn, (int)s.ncap,
+                       (const int*)s.iperm.p, (const unsigned char*)s.n_alive.p, (const long long*)s.n_supply.p,
+                       s.excess.p, s.p0.p, s.p1.p);
+    if (hi)
+        hipLaunchKernelGGL(k_reset_low, dim3(grid_for(hi)), dim3(BLK), 0, st, hi, (const unsigned char*)s.a_alive.p,
+                           (const int*)s.a_src.p, (const int*)s.a_dst.p, (const int*)s.perm.p,
+                           (const long long*)s.a_low.p, s.excess.p);
+    KS_CHECK(hipGetLastError());
+    return KS_OK;
+}
+
+int Engine::set_nodes(const NodeEdit* edits, size_t ne, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    return run_apply(s, edits, ne, nullptr, 0, err);
+}
+
+int Engine::task_pu(uint64_t* dev_out, size_t cap, size_t* count, int64_t n_tasks, std::string& err) {
+    EngineImpl& s = *p_;
+    if (!s.solved) {
+        err = "no successful solve";
+        return KS_E_INVALID;
+    }
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    *count = (size_t)n_tasks;
+    if (!dev_out || cap < (size_t)n_tasks || n_tasks == 0) {
+        if (dev_out && cap < (size_t)n_tasks) {
+            err = "output buffer smaller than the task count";
+            return KS_E_INVALID;
+        }
+        return KS_OK;
+    }
+    const int64_t m2 = std::max<int64_t>(s.m2cap, 1), ncap = s.ncap;
+    const int nn = s.nn;
+    KS_CHECK(s.map_outv.ensure(m2));
+    KS_CHECK(s.map_inv.ensure(m2));
+    KS_CHECK(s.map_outs.ensure(m2));
+    KS_CHECK(s.map_ins.ensure(m2));
+    KS_CHECK(s.map_itype.ensure(nn + 1));
+    KS_CHECK(s.map_rank.ensure(ncap + 1));
+    KS_CHECK(s.map_is_task.ensure(ncap + 1));
+    KS_CHECK(hipMemsetAsync(s.map_itype.p, 0, nn + 1, st));
+    if (s.m2cap)
+        hipLaunchKernelGGL(k_unit_vals, dim3(grid_for(s.m2cap)), dim3(BLK), 0, st, (long long)s.m2cap,
+                           (const int*)s.ent.p, (const long long*)s.flows.p, s.map_outv.p, s.map_inv.p);
+    hipLaunchKernelGGL(k_node_meta, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, (const int*)s.perm.p,
+                       (const unsigned char*)s.n_type.p, (const unsigned char*)s.n_alive.p, s.map_itype.p,
+                       s.map_is_task.p);
+    size_t t1 = 0, t2 = 0;
+    if (s.m2cap) KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.map_outv.p, s.map_outs.p, (int)s.m2cap, st));
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, s.map_is_task.p, s.map_rank.p, (int)ncap, st));
+    KS_CHECK(s.map_tmp.ensure(std::max(t1, t2)));
+    size_t tt = s.map_tmp.n;
+    if (s.m2cap) {
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_outv.p, s.map_outs.p, (int)s.m2cap, st));
+        tt = s.map_tmp.n;
+        KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_inv.p, s.map_ins.p, (int)s.m2cap, st));
+    }
+    tt = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_is_task.p, s.map_rank.p, (int)ncap, st));
+    hipLaunchKernelGGL(k_task_paths, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, nn, (const int*)s.perm.p,
+                       (const int*)s.first.p, (const int*)s.head.p, (const int*)s.rev.p,
+                       (const long long*)s.map_outv.p, (const long long*)s.map_outs.p,
+                       (const long long*)s.map_inv.p, (const long long*)s.map_ins.p, (const int*)s.iperm.p,
+                       (const unsigned char*)s.map_itype.p, (const int*)s.map_rank.p,
+                       (const int*)s.map_is_task.p, (unsigned long long*)dev_out);
+    KS_CHECK(hipGetLastError());
+    KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+int Engine::download(void* host_dst, const void* dev_src, size_t bytes, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    if (bytes) {
+        KS_CHECK(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, s.stream));
+        KS_CHECK(hipStreamSynchronize(s.stream));
+    }
+    return KS_OK;
+}
+
+int Engine::scratch(uint64_t** dev, size_t n, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    KS_CHECK(s.map_scratch.ensure(std::max<size_t>(1, n)));
+    *dev = s.map_scratch.p;
+    return KS_OK;
+}
+
+int Engine::flows(std::vector<ks_flow>& out, std::string& err) {
+    EngineImpl& s = *p_;
+    if (!s.solved) {
+        err = "no successful solve";
+        return KS_E_INVALID;
+    }
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    const int hi = s.hi();
+    out.clear();
+    if (!hi) return KS_OK;
+    KS_CHECK(s.flow_sel.ensure(hi));
+    KS_CHECK(s.flow_cnt.ensure(1));
+    hipcub::CountingInputIterator<int> it(0);
+    FlowPositive pred{s.a_alive.p, s.flows.p};
+    size_t t = 0;
+    KS_CHECK(hipcub::DeviceSelect::If(nullptr, t, it, s.flow_sel.p, s.flow_cnt.p, hi, pred, st));
+    KS_CHECK(s.map_tmp.ensure(std::max(t, s.map_tmp.n)));
+    t = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceSelect::If(s.map_tmp.p, t, it, s.flow_sel.p, s.flow_cnt.p, hi, pred, st));
+    int cnt = 0;
+    KS_CHECK(hipMemcpyAsync(&cnt, s.flow_cnt.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    if (!cnt) return KS_OK;
+    KS_CHECK(s.flow_recs.ensure(cnt));
+    hipLaunchKernelGGL(k_flow_records, dim3(grid_for(cnt)), dim3(BLK), 0, st, cnt, (const int*)s.flow_sel.p,
+                       (const int*)s.a_src.p, (const int*)s.a_dst.p, (const long long*)s.flows.p, s.flow_recs.p);
+    out.resize(cnt);
+    KS_CHECK(hipMemcpyAsync(out.data(), s.flow_recs.p, cnt * sizeof(ks_flow), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+static double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+    return ms;
+}
+
+int Engine::solve(ks_result& res, bool warm, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    const auto t_host0 = std::chrono::steady_clock::now();
+    auto wall_s = [&]() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count();
+    };
+    hipStream_t st = s.stream;
+    const bool use_warm = warm && s.has_prev;
+    s.solved = false;
+    res.warm_started = use_warm ? 1 : 0;
+    KS_CHECK(hipEventRecord(s.ev[0], st));
+    KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
+    KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
+    std::memset(s.h_ctl, 0, sizeof(Ctl));
+
+    // ------------------------------------------------- build / reset ---
+    // The CSR persists between solves; it is rebuilt from the arc table only when
+    // an in-place delta did not fit (or after a load). A cold solve resets the
+    // residual state; a warm one keeps it (carried across a rebuild by slot).
+    if (!s.csr_valid) {
+        const int64_t ncap_prev = s.ncap;
+        const long long mult_prev = s.mult;
+        const bool carry = use_warm && s.nn > 0;
+        const int hi0 = s.hi();
+        if (carry) {
+            KS_CHECK(s.saved_flows.ensure(std::max(hi0, 1)));
+            KS_CHECK(s.p_slot.ensure(std::max<int64_t>(ncap_prev, 1)));
+            if (hi0)
+                hipLaunchKernelGGL(k_save_flows, dim3(grid_for(hi0)), dim3(BLK), 0, st, hi0,
+                                   (const unsigned char*)s.a_alive.p, (const int*)s.fwd.p, (const int*)s.rev.p,
+                                   (const long long*)s.rcap.p, s.saved_flows.p);
+            hipLaunchKernelGGL(k_save_prices, dim3(grid_for(ncap_prev)), dim3(BLK), 0, st, (int)ncap_prev,
+                               (const int*)s.perm.p, (const long long*)s.p0.p, s.p_slot.p);
+        }
+        int rc = build(s, err);
+        if (rc) return rc;
+        rc = cold_reset(s, err);
+        if (rc) return rc;
+        if (carry) {
+            if (hi0)
+                hipLaunchKernelGGL(k_restore_flows, dim3(grid_for(hi0)), dim3(BLK), 0, st, hi0,
+                                   (const unsigned char*)s.a_alive.p, (const long long*)s.saved_flows.p,
+                                   (const long long*)s.a_low.p, (const long long*)s.a_cap.p, (const int*)s.fwd.p,
+                                   (const int*)s.rev.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
+                                   (const int*)s.perm.p, s.rcap.p, s.excess.p);
+            hipLaunchKernelGGL(k_restore_prices, dim3(grid_for(s.ncap)), dim3(BLK), 0, st, (int)s.ncap,
+                               (int)ncap_prev, mult_prev, s.mult, (const long long*)s.p_slot.p, (const int*)s.perm.p,
+                               s.p0.p, s.p1.p);
+        }
+    } else if (!use_warm) {
+        int rc = cold_reset(s, err);
+        if (rc) return rc;
+    }
+    const int hi = s.hi();
+    const int nn = s.nn;
+    const int64_t m2 = s.m2cap;
+    res.n_nodes = s.nslots;
+    res.n_arcs = s.h_sctl->live;
+    if (nn == 0) {
+        res.total_cost = 0;
+        res.flow_value = 0;   // no nodes: nothing flows
+        s.solved = true;
+        s.has_prev = true;
+        return KS_OK;
+    }
+    // max |cost| → the first phase's ε
+    if (hi)
+        hipLaunchKernelGGL(k_max_cost, dim3(grid_for(hi, 2048)), dim3(BLK), 0, st, hi,
+                           (const unsigned char*)s.a_alive.p, (const long long*)s.a_cost.p, &s.ctl.p->gu_L);
+    KS_CHECK(hipMemcpyAsync(s.h_ctl, s.ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    const long long maxc = s.h_ctl->gu_L;
+    KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
+    const long long mult = s.mult;
+    if (maxc > 0 && (double)maxc * (double)mult * 8.0 * (double)mult > 4.0e18) {
+        err = "cost range too large for int64 scaled prices";
+        return KS_E_RANGE;
+    }
     KS_CHECK(hipEventRecord(s.ev[1], st));
 
     // ------------------------------------------------------------ phases ---
-    const char* stamp_env = std::getenv("KS_STAMP");   // "sweep_index:path"
-    int stamp_at = -1;
-    std::string stamp_path;
-    if (stamp_env && *stamp_env && g_trace_ok(stamp_env, stamp_at, stamp_path)) {
-        KS_CHECK(s.stamps.ensure(3 * (size_t)(s.nhitems + s.ncitems / WPB + s.wbeg[NGC] / WPB + 64)));
-        KS_CHECK(hipMemsetAsync(s.stamps.p, 0, s.stamps.n * sizeof(unsigned long long), st));
-    }
     DG g = s.dg();
-    if (s.stamps.n > 1) g.stamp_sweep = stamp_at;
     {
         const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
         g.expand = ex ? std::atoi(ex) : 1;
@@ -2138,10 +2512,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
-    long long eps = std::max<long long>(1, (long long)s.maxc * mult);
-    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, cycles = 0, sweep_kernels = 0;
+    long long eps = std::max<long long>(1, maxc * mult);
+    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0;
     double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
-    int phases = 0, pr_skips = 0;
+    int phases = 0;
     int kb = 24;                        // Bellman-Ford rounds enqueued per cycle (adaptive)
     int sseq = 0, bseq = 0;             // frontier buffer sequences
     double ms_sat = 0, ms_cycles = 0, ms_pr = 0;
@@ -2193,22 +2567,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         return ok;
     };
 
-    // warm start: previous flows and prices, then start at a small ε (≤ K cost
-    // units, K = KS_WARM_K, default 8) and saturate only the arcs that violate it
+    // warm start: the previous flow and prices (in place), fresh nodes priced off
+    // their out-arcs, then a start at a small ε (≤ K cost units, K = KS_WARM_K,
+    // default 8) saturating only the arcs that violate it
     long long warm_thr = 0;
     if (use_warm) {
-        const int wgrid = grid_for(m, 2048);
-        if (m)
-            hipLaunchKernelGGL(k_warm_flows, dim3(wgrid), dim3(BLK), 0, st, (int)m,
-                               s.map_state == 2 ? (const int*)s.a_prev.p : (const int*)nullptr,
-                               (const long long*)s.prev_flows.p, (const long long*)s.a_low.p,
-                               (const long long*)s.a_cap.p, (const int*)s.fwd.p, (const int*)s.rev.p, s.rcap.p,
-                               (const int*)s.a_src.p, (const int*)s.a_dst.p, (const int*)s.perm.p, s.excess.p);
-        hipLaunchKernelGGL(k_warm_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n, (int)s.n_prev,
-                           s.mult_prev, mult, (const long long*)s.p_slot.p, (const int*)s.perm.p, s.p0.p, s.p1.p);
-        if (s.fresh_valid && s.map_state == 2)
-            hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n,
-                               (const unsigned char*)s.a_fresh.p, (const int*)s.perm.p, g);
+        hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
+                           (const unsigned char*)s.n_fresh.p, (const int*)s.perm.p, g);
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         KS_CHECK(read_ctl());
         long long K = 8;
@@ -2219,16 +2584,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         const long long e0 = std::max<long long>(1, std::min<long long>({viol, K * mult / D, eps}));
         warm_thr = e0;
         eps = e0 * alpha;   // the first phase runs at e0
+        KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
     }
 
     do {
         eps = std::max<long long>(1, eps / alpha);
         ++phases;
-        ptrace.push_back(PhaseRec{eps, sweep_launches, 0, {}, 0});
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g,
-                           phases == 1 && use_warm ? warm_thr : 0LL);
+        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 && use_warm ? warm_thr : 0LL);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         bool gu_running = false;
         uint64_t phase_sweeps = 0;
@@ -2240,7 +2604,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             if (new_gu) {
                 gu_r0 = s.h_ctl->bf_count;
                 hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g);
-                ptrace.back().gu_at.push_back(sweep_launches);
             }
             KS_CHECK(hipEventRecord(s.kev[0], st));
             bf_rounds(false, kb, new_gu);
@@ -2248,14 +2611,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             KS_CHECK(hipEventRecord(s.kev[2], st));
-            for (int k = 0; k < gi; ++k) {
-                const long long ti = (long long)sweep_launches + k;
-                hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k, sseq + k,
-                                   (g.trace && ti < kTraceMax) ? (int)ti : -1);
-            }
+            for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k, sseq + k);
             KS_CHECK(hipEventRecord(s.kev[3], st));
             KS_CHECK(read_ctl());
-            ++cycles;
             sweep_kernels += gi;
             ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
             ms_sw_k += ev_ms(s.kev[2], s.kev[3]);
@@ -2284,7 +2642,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
             }
-            if (phase_sweeps > (uint64_t)(64 * (n + 64)) || wall_s() > kSolveWallLimitS) {
+            if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
                       std::to_string(wall_s()) + " s)";
                 return KS_E_DEVICE;
@@ -2292,7 +2650,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
-        ptrace.back().end = sweep_launches;
         ms_sat += ev_ms(s.ev[2], s.ev[3]);
         ms_cycles += ev_ms(s.ev[3], s.ev[5]);
         if (status) break;
@@ -2302,11 +2659,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             int used = 0;
             int rc = price_refine(1, &used, pr_cap);
             if (rc < 0) return rc;
-            if (rc == 1) {
-                ++pr_skips;
-                eps = 1;
-                ptrace.push_back(PhaseRec{1, sweep_launches, sweep_launches, {}, used});
-            }
+            if (rc == 1) eps = 1;
         }
     } while (eps > 1);
 
@@ -2317,21 +2670,21 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
 
     // ------------------------------------------------------------ verify ---
     KS_CHECK(hipEventRecord(s.ev[6], st));
-    const int vgrid = grid_for(m, 2048);
+    const int vgrid = grid_for(hi, 2048);
     long long tot_cost = 0, tot_flow = 0;
     if (status == KS_OK) {
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
-        if (m) {
-            hipLaunchKernelGGL(k_verify_arcs, dim3(vgrid), dim3(BLK), 0, st, g, (const int*)s.fwd.p,
-                               (const int*)s.a_src.p, (const int*)s.a_dst.p, (const long long*)s.supply.p,
-                               (const long long*)s.a_low.p, (const long long*)s.a_cap.p,
-                               (const long long*)s.a_cost.p, s.flows.p, s.part.p, s.part.p + 4096);
-            hipLaunchKernelGGL(k_verify_opt, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
-        }
+        if (hi)
+            hipLaunchKernelGGL(k_verify_arcs, dim3(vgrid), dim3(BLK), 0, st, g, hi, (const unsigned char*)s.a_alive.p,
+                               (const int*)s.fwd.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
+                               (const long long*)s.n_supply.p, (const long long*)s.a_low.p,
+                               (const long long*)s.a_cap.p, (const long long*)s.a_cost.p, s.flows.p, s.part.p,
+                               s.part.p + 4096);
+        if (m2) hipLaunchKernelGGL(k_verify_opt, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         hipLaunchKernelGGL(k_verify_nodes, dim3(ngrid), dim3(BLK), 0, st, g);
-        std::vector<long long> parts(m ? vgrid : 0), partf(m ? vgrid : 0);
-        if (m) {
+        std::vector<long long> parts(hi ? vgrid : 0), partf(hi ? vgrid : 0);
+        if (hi) {
             KS_CHECK(hipMemcpyAsync(parts.data(), s.part.p, vgrid * sizeof(long long), hipMemcpyDeviceToHost, st));
             KS_CHECK(hipMemcpyAsync(partf.data(), s.part.p + 4096, vgrid * sizeof(long long), hipMemcpyDeviceToHost,
                                     st));
@@ -2354,39 +2707,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
 
-    if (trace_path && *trace_path && s.trace.n > 1) {
-        const uint64_t nt = std::min<uint64_t>(sweep_launches, kTraceMax);
-        std::vector<unsigned> ht(4 * nt);
-        if (nt) KS_CHECK(hipMemcpy(ht.data(), s.trace.p, 4 * nt * sizeof(unsigned), hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(trace_path, "a")) {
-            std::fprintf(f, "{\"n\": %lld, \"m\": %lld, \"phases\": [", (long long)n, (long long)m);
-            for (size_t i = 0; i < ptrace.size(); ++i) {
-                std::fprintf(f, "%s{\"eps\": %lld, \"begin\": %llu, \"end\": %llu, \"pr_rounds\": %d, \"gu_at\": [",
-                             i ? ", " : "", ptrace[i].eps, (unsigned long long)ptrace[i].begin,
-                             (unsigned long long)ptrace[i].end, ptrace[i].pr_rounds);
-                for (size_t k = 0; k < ptrace[i].gu_at.size(); ++k)
-                    std::fprintf(f, "%s%llu", k ? ", " : "", (unsigned long long)ptrace[i].gu_at[k]);
-                std::fprintf(f, "]}");
-            }
-            std::fprintf(f, "], ");
-            const char* names[4] = {"visits", "relabels", "groups", "heavy"};
-            for (int k = 0; k < 4; ++k) {
-                std::fprintf(f, "%s\"%s\": [", k ? "], " : "", names[k]);
-                for (uint64_t i = 0; i < nt; ++i) std::fprintf(f, "%s%u", i ? ", " : "", ht[4 * i + k]);
-            }
-            std::fprintf(f, "]}\n");
-            std::fclose(f);
-        }
-    }
-    if (s.stamps.n > 1 && !stamp_path.empty()) {
-        std::vector<unsigned long long> hs(s.stamps.n);
-        KS_CHECK(hipMemcpy(hs.data(), s.stamps.p, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(stamp_path.c_str(), "w")) {
-            for (size_t b = 0; b + 2 < hs.size(); b += 3)
-                if (hs[b]) std::fprintf(f, "%zu %llu %llu %llu\n", b / 3, hs[b], hs[b + 1], hs[b + 2]);
-            std::fclose(f);
-        }
-    }
     res.total_cost = tot_cost;
     res.flow_value = tot_flow;
     res.phases = phases;
@@ -2409,34 +2729,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.gu_launches = bf_launches;
     res.ms_gu_kernels = ms_bf_k;
     res.status = status;
-    (void)pr_skips;
-    (void)cycles;
     if (status == KS_OK) {
-        KS_CHECK(s.p_slot.ensure(n));
-        hipLaunchKernelGGL(k_save_prices, dim3(grid_for(n, 2048)), dim3(BLK), 0, st, (int)n, (const int*)s.perm.p,
-                           (const long long*)s.p0.p, s.p_slot.p);
+        KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
         KS_CHECK(hipStreamSynchronize(st));
         s.solved = true;
         s.has_prev = true;
-        s.map_state = 1;
-        s.n_prev = n;
-        s.mult_prev = mult;
+    } else {
+        s.has_prev = false;   // a failed solve leaves no usable warm state
     }
     return status;
-}
-
-int Engine::download_flows(int64_t* out, std::string& err) {
-    EngineImpl& s = *p_;
-    if (!s.solved) {
-        err = "no successful solve";
-        return KS_E_INVALID;
-    }
-    KS_CHECK(hipSetDevice(s.device));
-    if (s.m) {
-        KS_CHECK(hipMemcpyAsync(out, s.flows.p, s.m * sizeof(long long), hipMemcpyDeviceToHost, s.stream));
-        KS_CHECK(hipStreamSynchronize(s.stream));
-    }
-    return KS_OK;
 }
 
 }  // namespace ks

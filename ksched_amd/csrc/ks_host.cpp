@@ -7,9 +7,12 @@
 //   ks_solve          ↔ the Flowlessly solve
 //   ks_get_flows      ↔ the "f" lines consumed by readFlowGraph (:134-179)
 //   ks_get_task_mapping ↔ parseFlowToMapping (:183-269)
-// The graph store keeps ksched's node/arc semantics (flowgraph/graph.go:27-182):
-// NodeIDs index node slots directly, at most one arc per (src, dst), REMOVE_NODE
-// drops incident arcs. The device engine (ks_engine.hip) solves the compacted graph.
+// The graph itself lives on the device (ks_store.h): arc table, (src, dst) hash
+// index and residual CSR, edited in place by ks_apply_deltas. The host keeps only
+// node-level state — liveness, supply, type per NodeID (flowgraph/graph.go:27-182
+// semantics: ids index slots, REMOVE_NODE drops incident arcs, ids are reused) —
+// which is all a stream needs to be validated in order, sequentially, before the
+// device resolves it in parallel.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -28,26 +31,18 @@ struct NodeRec {
     int64_t excess = 0;
     int32_t type = 0;
     bool alive = false;
-    bool fresh = true;     // created since the last successful solve (warm start)
+    bool pad = false;
 };
 
-struct ArcRec {
-    uint64_t src = 0, dst = 0;
-    int64_t low = 0, cap = 0, cost = 0;
-    int32_t type = 0;
-    bool alive = false;
-    int prev_up = -1;      // index in the last solved upload; −1 = new since (warm start)
-};
 
 constexpr uint64_t kMaxId = (1ULL << 30);
 
 inline uint64_t arc_key(uint64_t s, uint64_t d) { return (s << 32) | d; }
 
-// (src, dst) → arc slot: open addressing with linear probing and backward-shift
-// deletion (no tombstones), power-of-two capacity kept under 1/2 load. Keys are
-// never 0 (node ids start at 1), so 0 marks an empty bucket. The incremental
-// stream of a scheduling round (~80k upserts/deletes at config 4) is dominated
-// by these lookups.
+// (src, dst) → record index for ks_coalesce_deltas: open addressing with linear
+// probing and backward-shift deletion (no tombstones), power-of-two capacity
+// kept under 1/2 load. Keys are never 0 (node ids start at 1), so 0 marks an
+// empty bucket.
 class ArcIndex {
 public:
     void clear() {
@@ -129,29 +124,23 @@ struct ks_ctx {
     std::string err;
 
     std::vector<NodeRec> nodes;            // index = NodeID (slot 0 unused)
-    std::vector<ArcRec> arcs;
-    std::vector<int> free_arcs;
-    ArcIndex arc_of;
-    std::vector<std::vector<int>> inc;     // per node: incident arc slots (lazy, see push_incident)
-    std::vector<uint32_t> live_deg;        // per node: live incident arcs
-    bool dirty = true;
-    bool reloaded = true;                  // ks_load_graph since the last solve: no warm start
-
-    // last upload (compact arrays) and solve outputs
-    std::vector<int> up_arc;               // compact index → arc slot
-    std::vector<int32_t> c_src, c_dst;
-    std::vector<int64_t> c_low, c_cap, c_cost, c_supply;
-    std::vector<int32_t> c_prev;
-    std::vector<uint8_t> c_fresh, c_type;
-    std::vector<int64_t> flows;
+    std::vector<uint32_t> epoch_of;        // per id: last apply that touched it
+    std::vector<int32_t> lastrm_of;        // per id: last REMOVE position in that apply
+    uint32_t epoch = 0;
+    int64_t sum_others = 0;                // Σ supply of live non-sink nodes
+    int64_t n_sinks = 0;
+    uint64_t sink_id = 0;                  // the sink (when n_sinks == 1)
+    int64_t n_tasks = 0;                   // live task nodes
+    int64_t dev_sink_supply = 0;           // the sink's supply as the device has it
     bool have_solution = false;
     bool flows_fresh = false;
-    int64_t n_slots = 0;
+    std::vector<ks_flow> flows;
 
     int fail(int code, const std::string& msg) {
         err = msg;
         return code;
     }
+    int64_t nslots() const { return (int64_t)nodes.size() - 1; }
 };
 
 namespace {
@@ -159,169 +148,36 @@ namespace {
 void ensure_node(ks_ctx* c, uint64_t id) {
     if (id >= c->nodes.size()) {
         c->nodes.resize(id + 1);
-        c->inc.resize(id + 1);
-        c->live_deg.resize(id + 1, 0);
+        c->epoch_of.resize(id + 1, 0);
+        c->lastrm_of.resize(id + 1, -1);
     }
 }
 
 bool node_alive(const ks_ctx* c, uint64_t id) { return id < c->nodes.size() && c->nodes[id].alive; }
 
-void kill_arc(ks_ctx* c, int slot) {
-    ArcRec& a = c->arcs[slot];
-    if (!a.alive) return;
-    a.alive = false;
-    a.prev_up = -1;
-    c->arc_of.erase(arc_key(a.src, a.dst));
-    c->free_arcs.push_back(slot);
-    --c->live_deg[a.src];
-    --c->live_deg[a.dst];
-}
-
-// Incidence lists are append-only between compactions: a killed arc's slot stays
-// in both endpoints' lists (and may later be reused by an arc of other nodes).
-// Long-lived hubs (sink, aggregators) would otherwise grow with history, so a
-// list is compacted to its live arcs once it exceeds twice its live degree.
-void push_incident(ks_ctx* c, uint64_t v, int slot) {
-    std::vector<int>& l = c->inc[v];
-    if (l.size() >= 2 * (size_t)c->live_deg[v] + 16) {
-        size_t k = 0;
-        for (int t : l) {
-            const ArcRec& a = c->arcs[t];
-            if (a.alive && (a.src == v || a.dst == v)) l[k++] = t;
-        }
-        l.resize(k);
-        std::sort(l.begin(), l.end());
-        l.erase(std::unique(l.begin(), l.end()), l.end());
+// Node-level aggregates (auto-sink demand, task count) follow every change.
+void account(ks_ctx* c, uint64_t id, const NodeRec& r, int sign) {
+    if (!r.alive) return;
+    if (r.type == KS_NODE_SINK) {
+        c->n_sinks += sign;
+        if (sign > 0) c->sink_id = id;
+    } else {
+        c->sum_others += sign * r.excess;
     }
-    l.push_back(slot);
+    if (r.type == KS_NODE_TASK) c->n_tasks += sign;
 }
 
-int upsert_arc(ks_ctx* c, uint64_t s, uint64_t d, int64_t low, int64_t cap, int64_t cost, int32_t type) {
+int check_arc(ks_ctx* c, uint64_t s, uint64_t d, uint64_t low, uint64_t cap, int64_t cost) {
+    if (s == 0 || d == 0 || s >= kMaxId || d >= kMaxId) return c->fail(KS_E_RANGE, "arc endpoint id out of range");
     if (!node_alive(c, s) || !node_alive(c, d))
         return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has a missing endpoint");
     if (s == d) return c->fail(KS_E_INVALID, "self-loop arc at node " + std::to_string(s));
-    if (low < 0 || cap < 0 || low > cap)
+    if (low > (uint64_t)INT64_MAX || cap > (uint64_t)INT64_MAX) return c->fail(KS_E_RANGE, "arc bound exceeds int64");
+    if (low > cap)
         return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has low > cap");
-    if (cap > (int64_t(1) << 53) || cost > (int64_t(1) << 40) || cost < -(int64_t(1) << 40))
+    if (cap > (uint64_t(1) << 53) || cost > (int64_t(1) << 40) || cost < -(int64_t(1) << 40))
         return c->fail(KS_E_RANGE, "arc capacity or cost outside the supported range");
-    int slot = c->arc_of.find(arc_key(s, d));
-    if (slot < 0) {
-        if (!c->free_arcs.empty()) {
-            slot = c->free_arcs.back();
-            c->free_arcs.pop_back();
-        } else {
-            slot = (int)c->arcs.size();
-            c->arcs.emplace_back();
-        }
-        c->arc_of.insert(arc_key(s, d), slot);
-        c->arcs[slot].prev_up = -1;
-        c->arcs[slot].alive = false;       // not yet: compaction below must skip it
-        push_incident(c, s, slot);
-        push_incident(c, d, slot);
-        ++c->live_deg[s];
-        ++c->live_deg[d];
-    }
-    ArcRec& a = c->arcs[slot];
-    a.src = s;
-    a.dst = d;
-    a.low = low;
-    a.cap = cap;
-    a.cost = cost;
-    a.type = type;
-    a.alive = true;
     return KS_OK;
-}
-
-int add_node(ks_ctx* c, uint64_t id, int64_t excess, int32_t type) {
-    if (id == 0 || id >= kMaxId) return c->fail(KS_E_RANGE, "node id " + std::to_string(id) + " out of range");
-    ensure_node(c, id);
-    if (c->nodes[id].alive)
-        return c->fail(KS_E_INVALID, "node " + std::to_string(id) + " already present");  // graph.go:95-98
-    c->nodes[id] = NodeRec{excess, type, true, true};
-    return KS_OK;
-}
-
-int remove_node(ks_ctx* c, uint64_t id) {
-    if (!node_alive(c, id)) return c->fail(KS_E_INVALID, "remove of missing node " + std::to_string(id));
-    for (int slot : c->inc[id]) {
-        const ArcRec& a = c->arcs[slot];
-        if (a.alive && (a.src == id || a.dst == id)) kill_arc(c, slot);
-    }
-    c->inc[id].clear();
-    c->live_deg[id] = 0;
-    c->nodes[id] = NodeRec{};
-    return KS_OK;
-}
-
-// Compact the live graph into device input arrays (node slot = id − 1).
-int upload(ks_ctx* c) {
-    uint64_t maxid = 0;
-    for (uint64_t id = c->nodes.size(); id-- > 1;)
-        if (c->nodes[id].alive) {
-            maxid = id;
-            break;
-        }
-    const int64_t n = (int64_t)maxid;
-    c->n_slots = n;
-    c->c_supply.assign(n, 0);
-    c->c_type.assign(n, 0);
-    int64_t others = 0;
-    int64_t sink = -1, nsinks = 0;
-    for (int64_t v = 0; v < n; ++v) {
-        const NodeRec& r = c->nodes[v + 1];
-        if (!r.alive) continue;
-        c->c_supply[v] = r.excess;
-        c->c_type[v] = (uint8_t)std::min<int32_t>(std::max<int32_t>(r.type, 0), 255);
-        if (r.type == KS_NODE_SINK) {
-            sink = v;
-            ++nsinks;
-        } else {
-            others += r.excess;
-        }
-    }
-    if (c->opts.auto_sink && nsinks == 1) c->c_supply[sink] = -others;
-    const bool warm = c->opts.warm_start && !c->reloaded;
-    const size_t live = c->arcs.size() - c->free_arcs.size();
-    c->up_arc.resize(live);
-    c->c_src.resize(live);
-    c->c_dst.resize(live);
-    c->c_low.resize(live);
-    c->c_cap.resize(live);
-    c->c_cost.resize(live);
-    c->c_prev.resize(warm ? live : 0);
-    size_t k = 0;
-    for (int slot = 0; slot < (int)c->arcs.size(); ++slot) {
-        const ArcRec& a = c->arcs[slot];
-        if (!a.alive) continue;
-        c->up_arc[k] = slot;
-        c->c_src[k] = (int32_t)(a.src - 1);
-        c->c_dst[k] = (int32_t)(a.dst - 1);
-        c->c_low[k] = a.low;
-        c->c_cap[k] = a.cap;
-        c->c_cost[k] = a.cost;
-        if (warm) c->c_prev[k] = a.prev_up;
-        ++k;
-    }
-    if (k != live) return c->fail(KS_E_INVALID, "internal: arc free list out of sync");
-    if (warm) {
-        c->c_fresh.assign(n, 0);
-        for (int64_t v = 0; v < n; ++v) c->c_fresh[v] = c->nodes[v + 1].alive && c->nodes[v + 1].fresh;
-    }
-    const int64_t m = (int64_t)c->up_arc.size();
-    int rc = c->eng.upload(n, m, c->c_src.data(), c->c_dst.data(), c->c_low.data(), c->c_cap.data(),
-                           c->c_cost.data(), c->c_supply.data(), c->c_type.data(), warm ? c->c_prev.data() : nullptr,
-                           warm ? c->c_fresh.data() : nullptr, c->err);
-    if (rc == KS_OK) c->dirty = false;
-    return rc;
-}
-
-int fetch_flows(ks_ctx* c) {
-    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
-    if (c->flows_fresh) return KS_OK;
-    c->flows.assign(c->up_arc.size(), 0);
-    int rc = c->eng.download_flows(c->flows.data(), c->err);
-    if (rc == KS_OK) c->flows_fresh = true;
-    return rc;
 }
 
 }  // namespace
@@ -352,8 +208,8 @@ ks_ctx* ks_create(int device, const ks_opts* opts) {
         return nullptr;
     }
     c->nodes.resize(1);
-    c->inc.resize(1);
-    c->live_deg.resize(1, 0);
+    c->epoch_of.resize(1, 0);
+    c->lastrm_of.resize(1, -1);
     return c;
 }
 
@@ -364,98 +220,143 @@ const char* ks_last_error(ks_ctx* c) { return c ? c->err.c_str() : "null context
 int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs, size_t m) {
     if (!c) return KS_E_INVALID;
     if ((n && !nodes) || (m && !arcs)) return c->fail(KS_E_INVALID, "null input array");
-    c->nodes.assign(1, NodeRec{});
-    c->inc.assign(1, {});
-    c->live_deg.assign(1, 0);
-    c->arcs.clear();
-    c->free_arcs.clear();
-    c->arc_of.clear();
-    c->arc_of.reserve(m);
-    c->arcs.reserve(m);
-    c->have_solution = false;
-    c->dirty = true;
-    c->reloaded = true;
     uint64_t maxid = 0;
-    for (size_t i = 0; i < n; ++i) maxid = std::max<uint64_t>(maxid, nodes[i].id);
-    if (maxid < kMaxId) {
-        c->nodes.reserve(maxid + 1);
-        c->inc.reserve(maxid + 1);
-        c->live_deg.reserve(maxid + 1);
-    }
     for (size_t i = 0; i < n; ++i) {
-        int rc = add_node(c, nodes[i].id, nodes[i].excess, nodes[i].type);
-        if (rc) return rc;
+        if (nodes[i].id == 0 || nodes[i].id >= kMaxId)
+            return c->fail(KS_E_RANGE, "node id " + std::to_string(nodes[i].id) + " out of range");
+        maxid = std::max<uint64_t>(maxid, nodes[i].id);
     }
-    {   // size the incidence lists once (one pass over the arcs)
-        std::vector<uint32_t> deg(c->nodes.size(), 0);
-        for (size_t i = 0; i < m; ++i) {
-            if (arcs[i].src < deg.size()) ++deg[arcs[i].src];
-            if (arcs[i].dst < deg.size()) ++deg[arcs[i].dst];
-        }
-        for (size_t v = 0; v < deg.size(); ++v)
-            if (deg[v]) c->inc[v].reserve(deg[v]);
+    std::vector<NodeRec> fresh(maxid + 1);
+    for (size_t i = 0; i < n; ++i) {
+        NodeRec& r = fresh[nodes[i].id];
+        if (r.alive)   // graph.go:95-98
+            return c->fail(KS_E_INVALID, "node " + std::to_string(nodes[i].id) + " already present");
+        r = NodeRec{nodes[i].excess, nodes[i].type, true, true};
     }
+    c->nodes.swap(fresh);
+    c->epoch_of.assign(maxid + 1, 0);
+    c->lastrm_of.assign(maxid + 1, -1);
+    c->sum_others = c->n_sinks = c->n_tasks = 0;
+    c->sink_id = 0;
+    for (uint64_t id = 1; id <= maxid; ++id) account(c, id, c->nodes[id], 1);
+    c->have_solution = false;
+    c->flows_fresh = false;
     for (size_t i = 0; i < m; ++i) {
         const ks_arc& a = arcs[i];
-        if (a.low > (uint64_t)INT64_MAX || a.cap > (uint64_t)INT64_MAX)
-            return c->fail(KS_E_RANGE, "arc bound exceeds int64");
-        int rc = upsert_arc(c, a.src, a.dst, (int64_t)a.low, (int64_t)a.cap, a.cost, a.type);
-        if (rc) return rc;
+        int rc = check_arc(c, a.src, a.dst, a.low, a.cap, a.cost);
+        if (rc) {
+            c->nodes.assign(1, NodeRec{});   // no half-loaded graph
+            c->sum_others = c->n_sinks = c->n_tasks = 0;
+            return rc;
+        }
     }
-    return KS_OK;
+    std::vector<int64_t> supply(maxid);
+    std::vector<uint8_t> type(maxid), alive(maxid);
+    for (uint64_t id = 1; id <= maxid; ++id) {
+        const NodeRec& r = c->nodes[id];
+        supply[id - 1] = r.alive ? r.excess : 0;
+        type[id - 1] = (uint8_t)std::min<int32_t>(std::max<int32_t>(r.type, 0), 255);
+        alive[id - 1] = r.alive ? 1 : 0;
+    }
+    c->dev_sink_supply = (c->n_sinks == 1) ? c->nodes[c->sink_id].excess : 0;
+    return c->eng.load((int64_t)maxid, supply.data(), type.data(), alive.data(), arcs, m, c->err);
 }
 
+// Validate the stream in order against node liveness (graph.go / the change
+// manager's preconditions), all or nothing: on an error the host state is rolled
+// back and nothing reaches the device. The device then resolves the records.
 int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     if (!c) return KS_E_INVALID;
     if (k && !d) return c->fail(KS_E_INVALID, "null delta array");
-    c->dirty = true;
-    c->have_solution = false;
-    for (size_t i = 0; i < k; ++i) {
+    if (k > (size_t)INT32_MAX) return c->fail(KS_E_RANGE, "delta stream too long");
+    if (++c->epoch == 0) {   // epoch wrapped: forget old stamps
+        std::fill(c->epoch_of.begin(), c->epoch_of.end(), 0);
+        c->epoch = 1;
+    }
+    std::vector<std::pair<uint64_t, NodeRec>> saved;   // first-touch state of every touched node
+    auto touch = [&](uint64_t id) {
+        ensure_node(c, id);
+        if (c->epoch_of[id] != c->epoch) {
+            c->epoch_of[id] = c->epoch;
+            c->lastrm_of[id] = -1;
+            saved.emplace_back(id, c->nodes[id]);
+        }
+    };
+    int rc = KS_OK;
+    for (size_t i = 0; i < k && rc == KS_OK; ++i) {
         const ks_delta& x = d[i];
-        int rc = KS_OK;
         switch (x.kind) {
             case KS_ADD_NODE:
-                rc = add_node(c, x.id, x.excess, x.type);
+                if (x.id == 0 || x.id >= kMaxId) {
+                    rc = c->fail(KS_E_RANGE, "node id " + std::to_string(x.id) + " out of range");
+                    break;
+                }
+                if (node_alive(c, x.id)) {   // graph.go:95-98
+                    rc = c->fail(KS_E_INVALID, "node " + std::to_string(x.id) + " already present");
+                    break;
+                }
+                touch(x.id);
+                c->nodes[x.id] = NodeRec{x.excess, x.type, true, true};
                 break;
             case KS_REMOVE_NODE:
-                rc = remove_node(c, x.id);
+                if (!node_alive(c, x.id)) {
+                    rc = c->fail(KS_E_INVALID, "remove of missing node " + std::to_string(x.id));
+                    break;
+                }
+                touch(x.id);
+                c->nodes[x.id] = NodeRec{};
+                c->lastrm_of[x.id] = (int32_t)i;
                 break;
             case KS_ADD_ARC:
-                if (x.low > (uint64_t)INT64_MAX || x.cap > (uint64_t)INT64_MAX) {
-                    rc = c->fail(KS_E_RANGE, "arc bound exceeds int64");
-                    break;
-                }
-                rc = upsert_arc(c, x.src, x.dst, (int64_t)x.low, (int64_t)x.cap, x.cost, x.type);
+                rc = check_arc(c, x.src, x.dst, x.low, x.cap, x.cost);
                 break;
-            case KS_UPDATE_ARC: {
-                if (x.src == 0 || x.dst == 0 || x.src >= kMaxId || x.dst >= kMaxId) {
-                    rc = c->fail(KS_E_RANGE, "arc endpoint id out of range");
-                    break;
-                }
-                if (x.low == 0 && x.cap == 0) {  // DeleteArc / ChangeArc(0,0): no capacity left
-                    const int slot = c->arc_of.find(arc_key(x.src, x.dst));
-                    if (slot >= 0) kill_arc(c, slot);
+            case KS_UPDATE_ARC:
+                if (x.low == 0 && x.cap == 0) {   // DeleteArc / ChangeArc(0,0): the arc goes
+                    if (x.src == 0 || x.dst == 0 || x.src >= kMaxId || x.dst >= kMaxId)
+                        rc = c->fail(KS_E_RANGE, "arc endpoint id out of range");
                     else if (!node_alive(c, x.src) || !node_alive(c, x.dst))
                         rc = c->fail(KS_E_INVALID, "update of arc with a missing endpoint");
                     break;
                 }
-                if (x.low > (uint64_t)INT64_MAX || x.cap > (uint64_t)INT64_MAX) {
-                    rc = c->fail(KS_E_RANGE, "arc bound exceeds int64");
+                rc = check_arc(c, x.src, x.dst, x.low, x.cap, x.cost);
+                break;
+            case KS_SET_EXCESS:
+                if (!node_alive(c, x.id)) {
+                    rc = c->fail(KS_E_INVALID, "excess of missing node " + std::to_string(x.id));
                     break;
                 }
-                rc = upsert_arc(c, x.src, x.dst, (int64_t)x.low, (int64_t)x.cap, x.cost, x.type);
-                break;
-            }
-            case KS_SET_EXCESS:
-                if (!node_alive(c, x.id)) rc = c->fail(KS_E_INVALID, "excess of missing node " + std::to_string(x.id));
-                else c->nodes[x.id].excess = x.excess;
+                touch(x.id);
+                c->nodes[x.id].excess = x.excess;
                 break;
             default:
                 rc = c->fail(KS_E_INVALID, "unknown delta kind " + std::to_string(x.kind));
         }
-        if (rc) return rc;
     }
-    return KS_OK;
+    if (rc) {   // roll back: the stream is applied entirely or not at all
+        for (auto it = saved.rbegin(); it != saved.rend(); ++it) c->nodes[it->first] = it->second;
+        return rc;
+    }
+    std::vector<ks::NodeEdit> edits;
+    edits.reserve(saved.size());
+    for (const auto& sv : saved) {
+        const uint64_t id = sv.first;
+        const NodeRec& now = c->nodes[id];
+        account(c, id, sv.second, -1);
+        account(c, id, now, 1);
+        ks::NodeEdit e;
+        std::memset(&e, 0, sizeof(e));
+        e.slot = (int32_t)(id - 1);
+        e.last_rm = c->lastrm_of[id];
+        e.supply = now.alive ? now.excess : 0;
+        e.alive = now.alive ? 1 : 0;
+        e.type = (uint8_t)std::min<int32_t>(std::max<int32_t>(now.type, 0), 255);
+        e.was_alive = sv.second.alive ? 1 : 0;
+        edits.push_back(e);
+        if (now.alive && now.type == KS_NODE_SINK) c->dev_sink_supply = now.excess;
+    }
+    c->have_solution = false;
+    c->flows_fresh = false;
+    return c->eng.apply(edits.data(), edits.size(), d, k, c->nslots(), c->err);
 }
 
 // Coalescing follows the store's semantics above: ADD_ARC and UPDATE_ARC are both
@@ -560,15 +461,22 @@ int ks_solve(ks_ctx* c, ks_result* out) {
     c->have_solution = false;
     c->flows_fresh = false;
     int rc = KS_OK;
-    if (c->dirty) rc = upload(c);
-    if (rc == KS_OK) rc = c->eng.solve(r, c->opts.warm_start != 0, c->err);
-    if (rc == KS_OK) {
-        // remember which upload index every arc had, for the next warm start
-        for (size_t i = 0; i < c->up_arc.size(); ++i) c->arcs[c->up_arc[i]].prev_up = (int)i;
-        for (auto& nd : c->nodes) nd.fresh = false;
-        c->reloaded = false;
-        c->have_solution = true;   // r.flow_value: measured on device from the resident flow
+    // auto-sink: the sink absorbs every other supply (its demand drifts without a
+    // message in the reference, graph_manager.go:640, 808)
+    if (c->opts.auto_sink && c->n_sinks == 1 && c->dev_sink_supply != -c->sum_others) {
+        ks::NodeEdit e;
+        std::memset(&e, 0, sizeof(e));
+        e.slot = (int32_t)(c->sink_id - 1);
+        e.last_rm = -1;
+        e.supply = -c->sum_others;
+        e.alive = 1;
+        e.type = KS_NODE_SINK;
+        e.was_alive = 1;
+        rc = c->eng.set_nodes(&e, 1, c->err);
+        if (rc == KS_OK) c->dev_sink_supply = -c->sum_others;
     }
+    if (rc == KS_OK) rc = c->eng.solve(r, c->opts.warm_start != 0, c->err);
+    if (rc == KS_OK) c->have_solution = true;   // r.flow_value: measured on device from the resident flow
     r.status = rc;
     if (out) *out = r;
     return rc;
@@ -596,43 +504,39 @@ int ks_solve_many(ks_ctx* const* ctxs, size_t k, int workers, ks_result* results
 
 int ks_get_flows(ks_ctx* c, ks_flow* out, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
-    int rc = fetch_flows(c);
-    if (rc) return rc;
-    size_t k = 0;
-    for (size_t i = 0; i < c->flows.size(); ++i)
-        if (c->flows[i] > 0) {
-            if (out && k < cap) {
-                const ArcRec& a = c->arcs[c->up_arc[i]];
-                out[k] = ks_flow{a.src, a.dst, c->flows[i]};
-            }
-            ++k;
-        }
-    *count = k;
+    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
+    if (!c->flows_fresh) {
+        int rc = c->eng.flows(c->flows, c->err);
+        if (rc) return rc;
+        c->flows_fresh = true;
+    }
+    if (out) std::memcpy(out, c->flows.data(), std::min(cap, c->flows.size()) * sizeof(ks_flow));
+    *count = c->flows.size();
     return KS_OK;
 }
 
-// Pairs from the device decomposition (Engine::task_pu): the i-th task slot in
-// slot order ↔ the i-th entry of the device vector.
+// Pairs from the device decomposition (Engine::task_pu): the i-th live task slot
+// in slot order ↔ the i-th entry of the device vector.
 int ks_get_task_mapping(ks_ctx* c, uint64_t* task, uint64_t* pu, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
     if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
     size_t nt = 0;
-    int rc = c->eng.task_pu(nullptr, 0, &nt, c->err);
+    int rc = c->eng.task_pu(nullptr, 0, &nt, c->n_tasks, c->err);
     if (rc) return rc;
     uint64_t* dev = nullptr;
     rc = c->eng.scratch(&dev, nt, c->err);
-    if (rc == KS_OK) rc = c->eng.task_pu(dev, nt, &nt, c->err);
+    if (rc == KS_OK) rc = c->eng.task_pu(dev, nt, &nt, c->n_tasks, c->err);
     std::vector<uint64_t> dense(nt);
     if (rc == KS_OK) rc = c->eng.download(dense.data(), dev, nt * sizeof(uint64_t), c->err);
     if (rc) return rc;
     size_t k = 0, ti = 0;
-    for (int64_t v = 0; v < c->n_slots && ti < nt; ++v) {
-        const NodeRec& r = c->nodes[v + 1];
+    for (uint64_t id = 1; id < c->nodes.size() && ti < nt; ++id) {
+        const NodeRec& r = c->nodes[id];
         if (!r.alive || r.type != KS_NODE_TASK) continue;
         const uint64_t p = dense[ti++];
         if (!p) continue;
         if (task && pu && k < cap) {
-            task[k] = (uint64_t)v + 1;
+            task[k] = id;
             pu[k] = p;
         }
         ++k;
@@ -644,7 +548,7 @@ int ks_get_task_mapping(ks_ctx* c, uint64_t* task, uint64_t* pu, size_t cap, siz
 int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
     if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
-    return c->eng.task_pu(dev_out, cap, count, c->err);
+    return c->eng.task_pu(dev_out, cap, count, c->n_tasks, c->err);
 }
 
 }  // extern "C"

@@ -1,0 +1,348 @@
+// ks_store.hip — on-device application of ksched's incremental change stream
+// (the k_apply_deltas of SURVEY §7; ks_store.h has the data model).
+//
+// A stream of k records is applied by six short kernels, all O(k) except the
+// liveness scan (O(arc slots), ≈ 10 µs at config 3):
+//   1. k_mark_removed     per node edit: its last REMOVE position (n_lastrm)
+//   2. k_hash_records     per arc record: find-or-insert its (src, dst) key with a
+//                         CAS into the open-addressing index; atomicMax of the
+//                         record position → the entry's LAST record
+//   3. k_kill_scan        per live arc slot touching a removed node: its flow goes
+//                         back to the endpoints' excess and its residual pair turns
+//                         inert; the slot is freed unless a record after the removal
+//                         re-creates the arc (then it is re-inserted in step 6)
+//   4. k_node_edits       per node edit: liveness, type, supply (excess follows)
+//   5. k_arc_deletes      per LAST record that deletes its arc (UPDATE 0/0) or that
+//                         a later removal of an endpoint kills
+//   6. k_arc_upserts      per LAST record that upserts: in-place edit of capacity,
+//                         bounds and cost (flow clamped, excess adjusted), or a new
+//                         arc inserted into free positions of both endpoints'
+//                         segments (atomicAdd on the segment fill counters; a full
+//                         segment raises ctl->overflow and the host rebuilds the CSR
+//                         from the arc table)
+// Superseded records (not the LAST for their key) do nothing: this is the
+// reference's mergeChangesToSameArc / removeDuplicateChanges /
+// purgeChangesBeforeNodeRemoval (graph_change_manager.go:220-279) done on device.
+// Deletes free slots (step 5) strictly before upserts allocate them (step 6):
+// the free-slot stack is never pushed and popped in the same kernel.
+#include "ks_store.h"
+
+namespace ks {
+namespace {
+
+constexpr int SBLK = 256;
+
+__device__ __forceinline__ unsigned hslot(unsigned long long k, int mask) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return (unsigned)k & (unsigned)mask;
+}
+
+// Index of key k's entry, inserting it (value −1) when absent. −1 if the table is full.
+__device__ int h_find_or_insert(const StoreDev& d, unsigned long long k) {
+    unsigned i = hslot(k, d.hmask);
+    for (int probe = 0; probe <= d.hmask; ++probe, i = (i + 1) & (unsigned)d.hmask) {
+        unsigned long long cur = __hip_atomic_load(&d.hkey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == k) return (int)i;
+        if (cur == HKEY_EMPTY) {
+            const unsigned long long was = atomicCAS(&d.hkey[i], HKEY_EMPTY, k);
+            if (was == HKEY_EMPTY || was == k) return (int)i;
+        }
+    }
+    return -1;
+}
+
+__device__ int h_find(const StoreDev& d, unsigned long long k) {
+    unsigned i = hslot(k, d.hmask);
+    for (int probe = 0; probe <= d.hmask; ++probe, i = (i + 1) & (unsigned)d.hmask) {
+        const unsigned long long cur = d.hkey[i];
+        if (cur == k) return (int)i;
+        if (cur == HKEY_EMPTY) return -1;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void h_tomb(const StoreDev& d, int e) {
+    if (e < 0) return;
+    const unsigned long long was = atomicExch(&d.hkey[e], HKEY_TOMB);
+    d.hval[e] = -1;
+    if (was != HKEY_TOMB) atomicAdd(&d.ctl->tombs, 1);
+}
+
+__device__ __forceinline__ void inert(const StoreDev& d, int p, int owner) {
+    d.ent[p] = -1;
+    d.rcap[p] = 0;
+    d.ucap[p] = 0;
+    d.scost[p] = DEAD_COST;
+    d.head[p] = owner;
+    d.rev[p] = p;
+}
+
+__device__ __forceinline__ int perm_of(const StoreDev& d, int slot) { return slot < d.ncap ? d.perm[slot] : -1; }
+
+// Return arc slot s's flow (and its lower bound) to its endpoints and make its
+// residual pair inert. Only when the CSR is valid and the arc has positions.
+__device__ void kill_positions(const StoreDev& d, int s) {
+    if (!d.csr_valid) return;
+    const int p = d.fwd[s];
+    if (p < 0) return;
+    d.fwd[s] = -1;
+    const int q = d.rev[p];
+    const long long f = d.rcap[q] + d.a_low[s];
+    const int xs = perm_of(d, d.a_src[s]), xd = perm_of(d, d.a_dst[s]);
+    if (f) {
+        atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)f);
+        atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)(-f));
+    }
+    inert(d, p, xs);
+    inert(d, q, xd);
+}
+
+__device__ __forceinline__ void free_slot(const StoreDev& d, int s) {
+    d.a_alive[s] = 0;
+    d.fwd[s] = -1;
+    const int t = atomicAdd(&d.ctl->free_top, 1);
+    d.free_stack[t] = s;
+    atomicSub(&d.ctl->live, 1);
+    atomicAdd(&d.ctl->killed, 1);
+}
+
+__device__ __forceinline__ bool is_arc_record(const ks_delta& x) {
+    return x.kind == KS_ADD_ARC || x.kind == KS_UPDATE_ARC;
+}
+
+// --------------------------------------------------------------- kernels ---
+__global__ void k_reset_counters(StoreDev d) {
+    if (threadIdx.x == 0) {
+        d.ctl->killed = d.ctl->inserted = d.ctl->updated = d.ctl->superseded = 0;
+    }
+}
+
+__global__ void k_mark_removed(StoreDev d, const NodeEdit* __restrict__ e, int ne, int value) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < ne; i += gridDim.x * SBLK)
+        if (e[i].last_rm >= 0) d.n_lastrm[e[i].slot] = value ? e[i].last_rm : -1;
+}
+
+__global__ void k_hash_records(StoreDev d, const ks_delta* __restrict__ r, int k, int* __restrict__ rec_ent) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
+        const ks_delta x = r[i];
+        int e = -1;
+        if (is_arc_record(x)) {
+            e = h_find_or_insert(d, arc_hkey((long long)x.src, (long long)x.dst));
+            if (e < 0) d.ctl->overflow |= 4;
+            else atomicMax(&d.hlast[e], i);
+        }
+        rec_ent[i] = e;
+    }
+}
+
+__global__ void k_kill_scan(StoreDev d, int hi) {
+    for (int s = blockIdx.x * SBLK + threadIdx.x; s < hi; s += gridDim.x * SBLK) {
+        if (!d.a_alive[s]) continue;
+        const int lr = max(d.n_lastrm[d.a_src[s]], d.n_lastrm[d.a_dst[s]]);
+        if (lr < 0) continue;
+        const int e = h_find(d, arc_hkey((long long)d.a_src[s] + 1, (long long)d.a_dst[s] + 1));
+        const int last = e >= 0 ? d.hlast[e] : -1;
+        kill_positions(d, s);
+        if (last < lr) {          // no record after the removal re-creates it
+            free_slot(d, s);
+            h_tomb(d, e);
+        }                         // else: alive with fwd = −1, re-inserted by k_arc_upserts
+    }
+}
+
+__global__ void k_reset_used(StoreDev d, const NodeEdit* __restrict__ e, int ne) {
+    if (!d.csr_valid) return;
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < ne; i += gridDim.x * SBLK) {
+        if (e[i].last_rm < 0 || !e[i].was_alive) continue;
+        const int x = perm_of(d, e[i].slot);
+        if (x >= 0) d.used[x] = 0;   // every incident arc is gone: the segment is free again
+    }
+}
+
+__global__ void k_node_edits(StoreDev d, const NodeEdit* __restrict__ e, int ne) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < ne; i += gridDim.x * SBLK) {
+        const NodeEdit x = e[i];
+        const long long sup = x.alive ? x.supply : 0;
+        const int p = perm_of(d, x.slot);
+        if (x.alive && p < 0) d.ctl->overflow |= 2;   // a node id beyond the build
+        if (d.csr_valid && p >= 0) {
+            if (x.last_rm >= 0 || !x.was_alive) d.excess[p] = sup;
+            else d.excess[p] += sup - d.n_supply[x.slot];
+        }
+        d.n_supply[x.slot] = sup;
+        d.n_alive[x.slot] = x.alive;
+        d.n_type[x.slot] = x.type;
+        if (x.alive && (x.last_rm >= 0 || !x.was_alive)) d.n_fresh[x.slot] = 1;
+    }
+}
+
+// Is record i (an arc record, the LAST for its key) killed by a later removal
+// of one of its endpoints?
+__device__ __forceinline__ bool killed_later(const StoreDev& d, const ks_delta& x, int i) {
+    return d.n_lastrm[x.src - 1] > i || d.n_lastrm[x.dst - 1] > i;
+}
+
+__global__ void k_arc_deletes(StoreDev d, const ks_delta* __restrict__ r, int k, const int* __restrict__ rec_ent) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
+        const int e = rec_ent[i];
+        if (e < 0) continue;
+        if (d.hlast[e] != i) {
+            atomicAdd(&d.ctl->superseded, 1);
+            continue;
+        }
+        const ks_delta x = r[i];
+        const bool del = x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0;
+        const bool dead = killed_later(d, x, i);
+        if (!del && !dead) continue;
+        const int s = d.hval[e];
+        if (s >= 0 && d.a_alive[s]) {   // (a slot killed by k_kill_scan is already free)
+            kill_positions(d, s);
+            free_slot(d, s);
+        }
+        h_tomb(d, e);
+    }
+}
+
+__global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k, const int* __restrict__ rec_ent) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
+        const int e = rec_ent[i];
+        if (e < 0 || d.hlast[e] != i) continue;
+        const ks_delta x = r[i];
+        if ((x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0) || killed_later(d, x, i)) continue;
+        int s = d.hval[e];
+        if (s < 0) {                    // a new arc: a free slot, else a fresh one
+            const int t = atomicSub(&d.ctl->free_top, 1) - 1;
+            if (t >= 0) s = d.free_stack[t];
+            else s = atomicAdd(&d.ctl->hi, 1);
+            if (s >= d.acap) {          // the host sizes the table first; never expected
+                d.ctl->overflow |= 8;
+                continue;
+            }
+            d.hval[e] = s;
+            d.a_alive[s] = 1;
+            d.fwd[s] = -1;
+            atomicAdd(&d.ctl->live, 1);
+        }
+        const int sl = (int)x.src - 1, dl = (int)x.dst - 1;
+        const long long low = (long long)x.low, cap = (long long)x.cap, u = cap - low;
+        const long long low_old = d.a_low[s];
+        d.a_src[s] = sl;
+        d.a_dst[s] = dl;
+        d.a_low[s] = low;
+        d.a_cap[s] = cap;
+        d.a_cost[s] = x.cost;
+        if (!d.csr_valid) continue;
+        const int xs = perm_of(d, sl), xd = perm_of(d, dl);
+        if (xs < 0 || xd < 0) {
+            d.ctl->overflow |= 2;
+            continue;
+        }
+        const int p0 = d.fwd[s];
+        if (p0 >= 0) {                  // in place: same endpoints, new bounds / cost
+            const int q0 = d.rev[p0];
+            const long long f = d.rcap[q0];
+            const long long fn = f < 0 ? 0 : (f > u ? u : f);
+            d.rcap[p0] = u - fn;
+            d.rcap[q0] = fn;
+            d.ucap[p0] = u;
+            d.ucap[q0] = u;
+            d.scost[p0] = x.cost * d.mult;
+            d.scost[q0] = -x.cost * d.mult;
+            const long long back = (f - fn) - (low - low_old);   // units returned to the tail
+            if (back) {
+                atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)back);
+                atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)(-back));
+            }
+            atomicAdd(&d.ctl->updated, 1);
+            continue;
+        }
+        const int ps = atomicAdd(&d.used[xs], 1), pd = atomicAdd(&d.used[xd], 1);
+        const int p = d.first[xs] + ps, q = d.first[xd] + pd;
+        if (p >= d.first[xs + 1] || q >= d.first[xd + 1]) {
+            d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
+            continue;
+        }
+        d.head[p] = xd;
+        d.rev[p] = q;
+        d.rcap[p] = u;
+        d.ucap[p] = u;
+        d.scost[p] = x.cost * d.mult;
+        d.ent[p] = 2 * s;
+        d.head[q] = xs;
+        d.rev[q] = p;
+        d.rcap[q] = 0;
+        d.ucap[q] = u;
+        d.scost[q] = -x.cost * d.mult;
+        d.ent[q] = 2 * s + 1;
+        d.fwd[s] = p;
+        if (low) {                      // lower-bound transform
+            atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)(-low));
+            atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)low);
+        }
+        atomicAdd(&d.ctl->inserted, 1);
+    }
+}
+
+__global__ void k_finish(StoreDev d, const int* __restrict__ rec_ent, int k) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
+        const int e = rec_ent[i];
+        if (e >= 0) d.hlast[e] = -1;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.ctl->free_top < 0) d.ctl->free_top = 0;
+}
+
+__global__ void k_hash_clear(StoreDev d) {
+    for (int i = blockIdx.x * SBLK + threadIdx.x; i <= d.hmask; i += gridDim.x * SBLK) {
+        d.hkey[i] = HKEY_EMPTY;
+        d.hval[i] = -1;
+        d.hlast[i] = -1;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->tombs = 0;
+}
+
+__global__ void k_hash_fill(StoreDev d, int hi) {
+    for (int s = blockIdx.x * SBLK + threadIdx.x; s < hi; s += gridDim.x * SBLK) {
+        if (!d.a_alive[s]) continue;
+        const int e = h_find_or_insert(d, arc_hkey((long long)d.a_src[s] + 1, (long long)d.a_dst[s] + 1));
+        if (e < 0) d.ctl->overflow |= 4;
+        else d.hval[e] = s;
+    }
+}
+
+inline int grid(long long n) {
+    long long b = (n + SBLK - 1) / SBLK;
+    return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+}  // namespace
+
+hipError_t store_apply(const StoreDev& d, const ks_delta* recs, int k, int* rec_ent, const NodeEdit* edits, int ne,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_reset_counters, dim3(1), dim3(64), 0, st, d);
+    if (ne) hipLaunchKernelGGL(k_mark_removed, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne, 1);
+    if (k) hipLaunchKernelGGL(k_hash_records, dim3(grid(k)), dim3(SBLK), 0, st, d, recs, k, rec_ent);
+    if (ne) {
+        hipLaunchKernelGGL(k_kill_scan, dim3(grid(d.acap)), dim3(SBLK), 0, st, d, d.acap);
+        hipLaunchKernelGGL(k_reset_used, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne);
+        hipLaunchKernelGGL(k_node_edits, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne);
+    }
+    if (k) {
+        hipLaunchKernelGGL(k_arc_deletes, dim3(grid(k)), dim3(SBLK), 0, st, d, recs, k, (const int*)rec_ent);
+        hipLaunchKernelGGL(k_arc_upserts, dim3(grid(k)), dim3(SBLK), 0, st, d, recs, k, (const int*)rec_ent);
+    }
+    hipLaunchKernelGGL(k_finish, dim3(grid(k)), dim3(SBLK), 0, st, d, (const int*)rec_ent, k);
+    if (ne) hipLaunchKernelGGL(k_mark_removed, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne, 0);
+    return hipGetLastError();
+}
+
+hipError_t store_rehash(const StoreDev& d, hipStream_t st) {
+    hipLaunchKernelGGL(k_hash_clear, dim3(grid((long long)d.hmask + 1)), dim3(SBLK), 0, st, d);
+    hipLaunchKernelGGL(k_hash_fill, dim3(grid(d.acap)), dim3(SBLK), 0, st, d, d.acap);
+    return hipGetLastError();
+}
+
+}  // namespace ks
