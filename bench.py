@@ -223,6 +223,7 @@ def run_incremental(args, D):
         ts = time.perf_counter()
         ctx.apply_deltas(d)
         ta = time.perf_counter()
+        sst = ctx.store_stats()
         r = ctx.solve()
         tb = time.perf_counter()
         mp = ctx.task_mapping()
@@ -235,7 +236,8 @@ def run_incremental(args, D):
                "warm": r.raw["warm_started"], "phases": r.raw["phases"], "sweeps": r.raw["sweeps"],
                "updates": r.raw["global_updates"], "bf_rounds": r.raw["gu_iterations"],
                "solve_parts_ms": {k: round(v, 2) for k, v in r.raw["ms"].items()},
-               "m": r.raw["n_arcs"], "running": int((cell.state == cell.RUN).sum())}
+               "m": r.raw["n_arcs"], "running": int((cell.state == cell.RUN).sum()),
+               "rebuilt": r.raw["rebuilt"], "store": {k: sst[k] for k in ("inserted", "updated", "killed", "superseded")}}
         if i >= args.warmup:
             t_total += dt
             results.append(r)

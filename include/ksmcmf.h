@@ -12,6 +12,10 @@
  *   ks_apply_deltas          placement/solver.go:118-123 writeIncremental →
  *                            dimacs/export.go:31-38 + the GenerateChange methods of
  *                            dimacs/{add_node,create_arc,update_arc,remove_node}_change.go
+ *                            — validated on the host, applied IN PLACE on the device:
+ *                            the graph (arc table, (src, dst) hash index, residual
+ *                            CSR with slack) stays resident in HBM between rounds; a
+ *                            stream is all-or-nothing (an invalid record applies none)
  *   ks_coalesce_deltas       the change optimisers graph_change_manager.go:220-279
  *                            (optimizeChanges: RemoveDuplicate, MergeToSameArc,
  *                            PurgeBeforeNodeRemoval — declared there, never implemented)
@@ -149,8 +153,21 @@ typedef struct ks_result {
     uint64_t gu_launches;      /* Bellman-Ford round launches (price updates, refinement)*/
     double   ms_gu_kernels;    /* HIP-event-timed span of all Bellman-Ford batches (ms)  */
     int32_t  warm_started;     /* 1 when this solve started from the previous solution   */
-    int32_t  reserved0;
+    int32_t  rebuilt;          /* 1 when this solve rebuilt the residual CSR from the arc
+                                  table (after a load, or a delta that did not fit)     */
 } ks_result;
+
+/* Counters of the device-resident graph store (ks_get_store_stats). */
+typedef struct ks_store_stats {
+    int64_t  live_arcs;        /* arcs in the store                                      */
+    int64_t  inserted;         /* last ks_apply_deltas: arcs inserted in place           */
+    int64_t  updated;          /*   arcs whose bounds / cost were edited in place        */
+    int64_t  killed;           /*   arcs removed (UPDATE 0/0 or an endpoint removed)     */
+    int64_t  superseded;       /*   records overridden by a later record for the arc     */
+    int64_t  rebuilds;         /* CSR rebuilds since ks_load_graph (1 = the load's own)  */
+    int64_t  residual_slots;   /* residual positions allocated (live pairs + slack)      */
+    int64_t  reserved[4];
+} ks_store_stats;
 
 typedef struct ks_flow {       /* one "f src dst flow" line                              */
     uint64_t src, dst;
@@ -209,6 +226,9 @@ int ks_get_task_mapping(ks_ctx* ctx, uint64_t* task, uint64_t* pu,
  * uint64 (KS_E_INVALID when cap < the task count); dev_out = NULL only sets
  * *count, the number of task nodes. */
 int ks_get_task_pu_device(ks_ctx* ctx, uint64_t* dev_out, size_t cap, size_t* count);
+
+/* Store counters (no device work). */
+int ks_get_store_stats(ks_ctx* ctx, ks_store_stats* out);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,7 @@ public:
     int download(void* host_dst, const void* dev_src, size_t bytes, std::string& err);
 
     int64_t live_arcs() const;
+    void store_stats(ks_store_stats* out) const;
     int device() const;
 
 private:

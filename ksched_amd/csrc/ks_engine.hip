@@ -1737,6 +1737,7 @@ struct EngineImpl {
     // ---- residual CSR built from the table (internal ids)
     bool csr_valid = false;   // CSR matches the table (deltas applied in place)
     bool incremental = false; // deltas seen since the load: rebuild with slack
+    int64_t rebuilds = 0;     // CSR builds since the load
     int64_t ncap = 0;         // node slots covered by the build
     long long mult = 1;       // cost multiplier (ncap + 1)
     int64_t m2cap = 0;        // residual positions (Σ segment capacities)
@@ -2050,6 +2051,7 @@ int Engine::load(int64_t nslots, const int64_t* supply, const uint8_t* type, con
     std::memset(s.h_sctl, 0, sizeof(StoreCtl));
     s.csr_valid = false;
     s.incremental = false;
+    s.rebuilds = 0;
     s.solved = false;
     s.has_prev = false;
     rc = ensure_arcs(s, (int64_t)m, err);
@@ -2087,6 +2089,19 @@ int Engine::apply(const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t
 }
 
 int64_t Engine::live_arcs() const { return p_->h_sctl ? p_->h_sctl->live : 0; }
+
+void Engine::store_stats(ks_store_stats* o) const {
+    const EngineImpl& s = *p_;
+    std::memset(o, 0, sizeof(*o));
+    if (!s.h_sctl) return;
+    o->live_arcs = s.h_sctl->live;
+    o->inserted = s.h_sctl->inserted;
+    o->updated = s.h_sctl->updated;
+    o->killed = s.h_sctl->killed;
+    o->superseded = s.h_sctl->superseded;
+    o->rebuilds = s.rebuilds;
+    o->residual_slots = s.m2cap;
+}
 
 // ------------------------------------------------------------------ build ---
 static int build(EngineImpl& s, std::string& err) {
@@ -2275,6 +2290,7 @@ static int build(EngineImpl& s, std::string& err) {
         KS_CHECK(hipStreamSynchronize(st));
     }
     s.csr_valid = true;
+    ++s.rebuilds;
     return KS_OK;
 }
 
@@ -2425,6 +2441,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const bool use_warm = warm && s.has_prev;
     s.solved = false;
     res.warm_started = use_warm ? 1 : 0;
+    res.rebuilt = s.csr_valid ? 0 : 1;
     KS_CHECK(hipEventRecord(s.ev[0], st));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));

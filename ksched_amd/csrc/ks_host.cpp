@@ -551,4 +551,10 @@ int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* coun
     return c->eng.task_pu(dev_out, cap, count, c->n_tasks, c->err);
 }
 
+int ks_get_store_stats(ks_ctx* c, ks_store_stats* out) {
+    if (!c || !out) return KS_E_INVALID;
+    c->eng.store_stats(out);
+    return KS_OK;
+}
+
 }  // extern "C"

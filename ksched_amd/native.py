@@ -19,7 +19,7 @@ KS_ADD_NODE, KS_REMOVE_NODE, KS_ADD_ARC, KS_UPDATE_ARC, KS_SET_EXCESS = 0, 1, 2,
 EXPORTED_SYMBOLS = (
     "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
     "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
-    "ks_coalesce_deltas",
+    "ks_coalesce_deltas", "ks_get_store_stats",
 )
 
 NODE_DT = np.dtype({"names": ["id", "excess", "type", "_pad"],
@@ -48,13 +48,22 @@ class KsResult(C.Structure):
                 ("ms_phase", C.c_double * 6), ("n_nodes", C.c_int64), ("n_arcs", C.c_int64),
                 ("sweep_launches", C.c_uint64), ("ms_sweep_kernels", C.c_double),
                 ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double), ("warm_started", C.c_int32),
-                ("reserved0", C.c_int32)]
+                ("rebuilt", C.c_int32)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ms_phase"}
         names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d
+
+
+class KsStoreStats(C.Structure):
+    _fields_ = [("live_arcs", C.c_int64), ("inserted", C.c_int64), ("updated", C.c_int64),
+                ("killed", C.c_int64), ("superseded", C.c_int64), ("rebuilds", C.c_int64),
+                ("residual_slots", C.c_int64), ("reserved", C.c_int64 * 4)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class KsError(RuntimeError):
@@ -108,6 +117,7 @@ def load(build_if_missing: bool = True):
     L.ks_get_task_pu_device.argtypes = [V, V, C.c_size_t, P(C.c_size_t)]
     L.ks_solve_many.argtypes = [P(V), C.c_size_t, C.c_int, P(KsResult)]
     L.ks_coalesce_deltas.argtypes = [V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]
+    L.ks_get_store_stats.argtypes = [V, P(KsStoreStats)]
     _LIB = L
     return L
 
@@ -203,6 +213,11 @@ class Context:
         p = np.zeros(cnt.value, np.uint64)
         self._check(self._L.ks_get_task_mapping(self._h, t.ctypes.data, p.ctypes.data, cnt.value, C.byref(cnt)))
         return dict(zip(t.tolist(), p.tolist()))
+
+    def store_stats(self) -> dict:
+        st = KsStoreStats()
+        self._check(self._L.ks_get_store_stats(self._h, C.byref(st)))
+        return st.as_dict()
 
     def task_pu_device(self, dev_ptr: int, cap: int) -> int:
         cnt = C.c_size_t()

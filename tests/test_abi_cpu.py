@@ -53,14 +53,16 @@ LAYOUT_C = r"""
 #include "ksmcmf.h"
 #define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F))
 int main(void) {
-  printf("ks_opts %zu\nks_node %zu\nks_arc %zu\nks_delta %zu\nks_result %zu\nks_flow %zu\n",
-         sizeof(ks_opts), sizeof(ks_node), sizeof(ks_arc), sizeof(ks_delta), sizeof(ks_result), sizeof(ks_flow));
+  printf("ks_opts %zu\nks_node %zu\nks_arc %zu\nks_delta %zu\nks_result %zu\nks_flow %zu\nks_store_stats %zu\n",
+         sizeof(ks_opts), sizeof(ks_node), sizeof(ks_arc), sizeof(ks_delta), sizeof(ks_result), sizeof(ks_flow),
+         sizeof(ks_store_stats));
   P(ks_node, excess); P(ks_node, type);
   P(ks_arc, dst); P(ks_arc, low); P(ks_arc, cap); P(ks_arc, cost); P(ks_arc, type);
   P(ks_delta, id); P(ks_delta, src); P(ks_delta, dst); P(ks_delta, low); P(ks_delta, cap);
   P(ks_delta, cost); P(ks_delta, old_cost); P(ks_delta, excess);
   P(ks_result, status); P(ks_result, sweeps); P(ks_result, ms_phase); P(ks_result, n_nodes);
-  P(ks_result, ms_gu_kernels);
+  P(ks_result, ms_gu_kernels); P(ks_result, rebuilt);
+  P(ks_store_stats, superseded); P(ks_store_stats, residual_slots);
   P(ks_flow, flow);
   return 0;
 }
@@ -81,13 +83,16 @@ def test_struct_layouts_match_bindings(tmp_path):
     assert out["ks_arc"] == native.ARC_DT.itemsize
     assert out["ks_delta"] == native.DELTA_DT.itemsize
     assert out["ks_flow"] == native.FLOW_DT.itemsize
+    assert out["ks_store_stats"] == C.sizeof(native.KsStoreStats)
+    for f in ("superseded", "residual_slots"):
+        assert getattr(native.KsStoreStats, f).offset == out[f"ks_store_stats.{f}"], f
     for dt, cname in ((native.NODE_DT, "ks_node"), (native.ARC_DT, "ks_arc"), (native.DELTA_DT, "ks_delta"),
                       (native.FLOW_DT, "ks_flow")):
         for f in dt.names:
             key = f"{cname}.{f}"
             if key in out:
                 assert dt.fields[f][1] == out[key], key
-    for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels"):
+    for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels", "rebuilt"):
         assert getattr(native.KsResult, f).offset == out[f"ks_result.{f}"], f
 
 
