@@ -230,6 +230,61 @@ int ks_get_task_pu_device(ks_ctx* ctx, uint64_t* dev_out, size_t cap, size_t* co
 /* Store counters (no device work). */
 int ks_get_store_stats(ks_ctx* ctx, ks_store_stats* out);
 
+/* ---- scheduler-side sweeps of a round, on the device-resident graph ------- */
+
+/* pb.SchedulingDelta_ChangeType (proto/scheduling_delta.proto:11-16) */
+#define KS_DELTA_PLACE   0
+#define KS_DELTA_PREEMPT 1
+#define KS_DELTA_MIGRATE 2
+#define KS_DELTA_NOOP    3
+
+typedef struct ks_sched_delta {
+    int32_t  type;             /* KS_DELTA_*                                             */
+    int32_t  _pad;
+    uint64_t task;             /* task NodeID                                            */
+    uint64_t pu;               /* PU NodeID (PLACE / MIGRATE: the new one; PREEMPT: the
+                                  one it leaves)                                         */
+} ks_sched_delta;
+
+/* Seed the device-kept task bindings (TaskBindings, flowscheduler/scheduler.go:421-437):
+ * task NodeID → bound PU NodeID (0 = unbind). A REMOVE_NODE of a task unbinds it. */
+int ks_set_bindings(ks_ctx* ctx, const uint64_t* task, const uint64_t* pu, size_t k);
+
+/* Scheduling deltas of the last solve against the bindings, on device:
+ * SchedulingDeltasForPreemptedTasks (graph_manager.go:297-339) — a bound task absent
+ * from the mapping → PREEMPT, emitted first — then NodeBindingToSchedulingDelta
+ * (:253-295) per mapped task: unbound → PLACE, bound elsewhere → MIGRATE, bound here
+ * → nothing; each in task-id order. Every destination must be a PU (:259-262),
+ * else KS_E_VERIFY. commit != 0 applies the deltas to the bindings
+ * (applySchedulingDeltas, scheduler.go:377-412). out == NULL: *count only, nothing
+ * committed; otherwise cap ≥ the count is required (KS_E_INVALID, nothing committed). */
+int ks_scheduling_deltas(ks_ctx* ctx, int commit, ks_sched_delta* out, size_t cap, size_t* count);
+
+#define KS_COST_SET 0
+#define KS_COST_ADD 1
+
+/* UpdateAllCostsToUnscheduledAggs (graph_manager.go:462-475, called by Solve before
+ * every incremental export, solver.go:86) on device, in place: for every task with
+ * an arc into an unscheduled aggregator, a running task (it has a running arc,
+ * type 1) gets its running arc set to continuation_cost (TaskContinuationCost),
+ * any other task its arc to the aggregator set to (KS_COST_SET) or raised by
+ * (KS_COST_ADD: waiting-time ageing) unsched_cost (TaskToUnscheduledAggCost).
+ * Aggregators: unsched_ids (k of them), or with unsched_ids == NULL every type-0
+ * node with an arc into the sink. *changed (may be NULL) = arcs whose cost changed. */
+int ks_update_unsched_costs(ks_ctx* ctx, const uint64_t* unsched_ids, size_t k, int32_t mode,
+                            int64_t unsched_cost, int64_t continuation_cost, size_t* changed);
+
+/* ComputeTopologyStatistics (graph_manager.go:480-511; trivial model PrepareStats /
+ * GatherStats, costmodel/trivial_cost_modeler.go:147-176) on device: BFS from the
+ * sink over in-arcs; a PU takes (len(CurrentRunningTasks), max_tasks_per_pu), every
+ * resource node above sums its children. CurrentRunningTasks lengths: pu_running[i]
+ * for PU pu_ids[i] (k of them), or with pu_ids == NULL the running arcs (type 1)
+ * into each PU. Writes slots_below[id-1] / running_below[id-1] for ids 1..*count
+ * (0 for nodes that are not resources); cap < *count → KS_E_INVALID. */
+int ks_topology_stats(ks_ctx* ctx, uint64_t max_tasks_per_pu, const uint64_t* pu_ids,
+                      const uint64_t* pu_running, size_t k, uint64_t* slots_below,
+                      uint64_t* running_below, size_t cap, size_t* count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,8 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libksmcmf.so")
-SOURCES = [os.path.join(CSRC, "ks_engine.hip"), os.path.join(CSRC, "ks_store.hip"), os.path.join(CSRC, "ks_host.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "ks_engine.h"), os.path.join(CSRC, "ks_store.h"),
+SOURCES = [os.path.join(CSRC, f) for f in ("ks_engine.hip", "ks_store.hip", "ks_sched.hip", "ks_host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "ks_engine.h"), os.path.join(CSRC, "ks_store.h"), os.path.join(CSRC, "ks_sched.h"),
                   os.path.join(ROOT, "include", "ksmcmf.h")]
 
 

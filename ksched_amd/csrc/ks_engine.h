@@ -59,7 +59,16 @@ public:
     int download(void* host_dst, const void* dev_src, size_t bytes, std::string& err);
 
     int64_t live_arcs() const;
+    bool solved() const;
     void store_stats(ks_store_stats* out) const;
+
+    // Scheduler-side sweeps of a round (ks_sched.hip); see include/ksmcmf.h.
+    int set_bindings(const uint64_t* task, const uint64_t* pu, size_t k, std::string& err);
+    int sched_deltas(int commit, std::vector<ks_sched_delta>* out, size_t* count, int64_t n_tasks, std::string& err);
+    int unsched_costs(const uint64_t* ids, size_t k, int mode, int64_t ucost, int64_t ccost, size_t* changed,
+                      std::string& err);
+    int topology_stats(uint64_t mtpp, const uint64_t* pu_ids, const uint64_t* pu_running, size_t k, int64_t sink_slot,
+                       uint64_t* slots_below, uint64_t* running_below, std::string& err);
     int device() const;
 
 private:

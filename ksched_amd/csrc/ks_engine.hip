@@ -57,6 +57,7 @@
 #include <vector>
 
 #include "ks_engine.h"
+#include "ks_sched.h"
 
 namespace ks {
 namespace {
@@ -441,14 +442,19 @@ __global__ void k_degree(int hi, const unsigned char* __restrict__ alive, const 
         }
 }
 
-// Segment capacity of a node slot: its degree; with slack (incremental mode)
-// +25 % (at least 2) rounded up to a lane group (≤ 64) or a 64-arc chunk, and
-// one 8-lane group for dead or spare slots (room for a task id that is reused,
-// flowgraph/graph.go:169-182).
-__host__ __device__ inline int seg_capacity(int deg, bool alive, int slack) {
+// Segment capacity of a node slot. Tight after a load (its degree). Once the
+// graph is edited incrementally: tasks (≤ 8 arcs: preferences, or one running
+// arc after the pin) one 8-lane group — a removed task's segment is reused
+// whole by the task that takes over its id (flowgraph/graph.go:169-182), and
+// so are dead and spare slots; other nodes their degree +50 % (at least 4)
+// rounded up to a lane group (≤ 64) or a 64-arc chunk, never less than what
+// they had before (hint) unless that is 4× their need — an aggregator whose
+// degree fell after the pins keeps room for the next arrivals — and twice that
+// when an insert overflowed them since the last build.
+__host__ __device__ inline int seg_capacity(int deg, bool alive, bool task, int slack) {
     if (!slack) return deg;
-    if (!alive && deg == 0) return 8;
-    const int c = deg + (deg / 4 > 2 ? deg / 4 : 2);
+    if ((!alive || task) && deg <= 8) return 8;
+    const int c = deg + (deg / 2 > 4 ? deg / 2 : 4);
     if (c <= 64) {
         int g = 4;
         while (g < c) g <<= 1;
@@ -458,11 +464,21 @@ __host__ __device__ inline int seg_capacity(int deg, bool alive, int slack) {
 }
 
 __global__ void k_capacity(int ncap, int nstore, const int* __restrict__ deg, const unsigned char* __restrict__ alive,
-                           int slack, int* __restrict__ capv, unsigned char* __restrict__ cls) {
+                           const unsigned char* __restrict__ type, int slack, int* __restrict__ hint,
+                           unsigned char* __restrict__ grow, int* __restrict__ capv, unsigned char* __restrict__ cls) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
         const int d = v < nstore ? deg[v] : 0;
         const bool a = v < nstore && alive[v];
-        const int c = seg_capacity(d, a, slack);
+        int c = seg_capacity(d, a, a && type[v] == KS_NODE_TASK, slack);
+        if (slack && v < nstore) {
+            const int h = hint[v];
+            if (grow[v]) c = max(c, 2 * max(h, 4));
+            else if (h <= 4 * c) c = max(c, h);
+            else c = max(c, h / 2);
+            if (c > 64) c = (c + 63) / 64 * 64;
+            grow[v] = 0;
+        }
+        if (v < nstore) hint[v] = c;
         capv[v] = c;
         cls[v] = (unsigned char)degree_class(c);
     }
@@ -1721,11 +1737,14 @@ struct EngineImpl {
     DBuf<long long> n_supply;
     DBuf<unsigned char> n_type, n_alive, n_fresh;
     DBuf<int> n_lastrm;
+    DBuf<int> n_hint;         // per slot: segment capacity of the last build
+    DBuf<unsigned char> n_grow;
+    DBuf<unsigned long long> n_bind;   // per slot: bound PU (scheduling deltas)
     // ---- arc table (by slot) and its hash index
     int64_t acap = 0;
     DBuf<int> a_src, a_dst, fwd, free_stack;
     DBuf<long long> a_low, a_cap, a_cost;
-    DBuf<unsigned char> a_alive;
+    DBuf<unsigned char> a_alive, a_type;
     int64_t hcap = 0;
     DBuf<unsigned long long> hkey;
     DBuf<int> hval, hlast;
@@ -1773,6 +1792,37 @@ struct EngineImpl {
     DBuf<unsigned char> map_itype, map_tmp;
     DBuf<uint64_t> map_scratch;  // device vector behind ks_get_task_mapping
     DBuf<ks_flow> flow_recs;
+    // ---- scheduler-side sweeps (ks_sched.hip)
+    DBuf<int> sched_i;                  // int scratch
+    DBuf<unsigned long long> sched_u;   // u64 scratch
+    DBuf<unsigned char> sched_b;        // byte scratch
+    DBuf<ks_sched_delta> sched_d;
+
+    SchedDev schd() const {
+        SchedDev d{};
+        d.ncap = (int)ncap;
+        d.nstore = nstore;
+        d.perm = perm.p;
+        d.iperm = iperm.p;
+        d.n_alive = n_alive.p;
+        d.n_type = n_type.p;
+        d.n_bind = n_bind.p;
+        d.hi = h_sctl ? h_sctl->hi : 0;
+        d.a_alive = a_alive.p;
+        d.a_type = a_type.p;
+        d.a_src = a_src.p;
+        d.a_dst = a_dst.p;
+        d.a_cost = a_cost.p;
+        d.fwd = fwd.p;
+        d.first = first.p;
+        d.head = head.p;
+        d.rev = rev.p;
+        d.ent = ent.p;
+        d.scost = scost.p;
+        d.mult = mult;
+        d.csr_valid = csr_valid ? 1 : 0;
+        return d;
+    }
 
     ~EngineImpl() {
         if (stream) {
@@ -1780,6 +1830,8 @@ struct EngineImpl {
             (void)hipStreamSynchronize(stream);
         }
         n_supply.release(); n_type.release(); n_alive.release(); n_fresh.release(); n_lastrm.release();
+        n_hint.release(); n_grow.release(); n_bind.release(); a_type.release(); sched_i.release(); sched_u.release();
+        sched_b.release(); sched_d.release();
         a_src.release(); a_dst.release(); fwd.release(); free_stack.release(); a_low.release(); a_cap.release();
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
@@ -1812,6 +1864,8 @@ struct EngineImpl {
         d.n_alive = n_alive.p;
         d.n_fresh = n_fresh.p;
         d.n_lastrm = n_lastrm.p;
+        d.n_grow = n_grow.p;
+        d.n_bind = n_bind.p;
         d.perm = perm.p;
         d.acap = (int)acap;
         d.a_src = a_src.p;
@@ -1819,6 +1873,7 @@ struct EngineImpl {
         d.a_low = a_low.p;
         d.a_cap = a_cap.p;
         d.a_cost = a_cost.p;
+        d.a_type = a_type.p;
         d.a_alive = a_alive.p;
         d.fwd = fwd.p;
         d.free_stack = free_stack.p;
@@ -1946,6 +2001,9 @@ static int ensure_nodes(EngineImpl& s, int64_t need, std::string& err) {
     KS_CHECK(s.n_alive.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_fresh.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_lastrm.grow(cap, s.nstore, 0xff, st));
+    KS_CHECK(s.n_hint.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_grow.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_bind.grow(cap, s.nstore, 0, st));
     s.nstore = cap;
     return KS_OK;
 }
@@ -1966,6 +2024,7 @@ static int ensure_arcs(EngineImpl& s, int64_t need, std::string& err) {
     KS_CHECK(s.a_cap.grow(cap, keep, 0, st));
     KS_CHECK(s.a_cost.grow(cap, keep, 0, st));
     KS_CHECK(s.a_alive.grow(cap, keep, 0, st));
+    KS_CHECK(s.a_type.grow(cap, keep, 0, st));
     KS_CHECK(s.fwd.grow(cap, keep, 0xff, st));
     KS_CHECK(s.free_stack.grow(cap, keep, 0, st));
     KS_CHECK(s.flows.grow(cap, keep, 0, st));
@@ -2037,6 +2096,9 @@ int Engine::load(int64_t nslots, const int64_t* supply, const uint8_t* type, con
     KS_CHECK(hipMemsetAsync(s.n_supply.p, 0, s.nstore * sizeof(long long), st));
     KS_CHECK(hipMemsetAsync(s.n_type.p, 0, s.nstore, st));
     KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
+    KS_CHECK(hipMemsetAsync(s.n_hint.p, 0, s.nstore * sizeof(int), st));
+    KS_CHECK(hipMemsetAsync(s.n_grow.p, 0, s.nstore, st));
+    KS_CHECK(hipMemsetAsync(s.n_bind.p, 0, s.nstore * sizeof(unsigned long long), st));
     if (nslots) {
         KS_CHECK(hipMemcpyAsync(s.n_supply.p, supply, nslots * sizeof(long long), hipMemcpyHostToDevice, st));
         KS_CHECK(hipMemcpyAsync(s.n_type.p, type, nslots, hipMemcpyHostToDevice, st));
@@ -2089,6 +2151,7 @@ int Engine::apply(const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t
 }
 
 int64_t Engine::live_arcs() const { return p_->h_sctl ? p_->h_sctl->live : 0; }
+bool Engine::solved() const { return p_->solved; }
 
 void Engine::store_stats(ks_store_stats* o) const {
     const EngineImpl& s = *p_;
@@ -2126,7 +2189,9 @@ static int build(EngineImpl& s, std::string& err) {
         hipLaunchKernelGGL(k_degree, dim3(grid_for(hi)), dim3(BLK), 0, st, hi, (const unsigned char*)s.a_alive.p,
                            (const int*)s.a_src.p, (const int*)s.a_dst.p, s.deg.p);
     hipLaunchKernelGGL(k_capacity, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, (int)s.nstore,
-                       (const int*)s.deg.p, (const unsigned char*)s.n_alive.p, s.incremental ? 1 : 0, s.capv.p, s.cls.p);
+                       (const int*)s.deg.p, (const unsigned char*)s.n_alive.p, (const unsigned char*)s.n_type.p,
+                       s.incremental ? 1 : 0, s.n_hint.p,
+                       s.n_grow.p, s.capv.p, s.cls.p);
     {
         hipcub::CountingInputIterator<int> it(0);
         size_t tmp = 0, t2 = 0;
@@ -2421,6 +2486,181 @@ int Engine::flows(std::vector<ks_flow>& out, std::string& err) {
     out.resize(cnt);
     KS_CHECK(hipMemcpyAsync(out.data(), s.flow_recs.p, cnt * sizeof(ks_flow), hipMemcpyDeviceToHost, st));
     KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+// ------------------------------------------------- scheduler-side sweeps ---
+int Engine::set_bindings(const uint64_t* task, const uint64_t* pu, size_t k, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    if (!k) return KS_OK;
+    std::vector<unsigned long long> ids(task, task + k), vals(pu, pu + k);
+    for (size_t i = 0; i < k; ++i)
+        if (ids[i] == 0 || (int64_t)ids[i] > s.nstore) {
+            err = "binding for a task id beyond the graph";
+            return KS_E_INVALID;
+        }
+    KS_CHECK(s.sched_u.ensure(2 * k));
+    hipStream_t st = s.stream;
+    KS_CHECK(hipMemcpyAsync(s.sched_u.p, ids.data(), k * 8, hipMemcpyHostToDevice, st));
+    KS_CHECK(hipMemcpyAsync(s.sched_u.p + k, vals.data(), k * 8, hipMemcpyHostToDevice, st));
+    // the same scatter as the running counts: n_bind[id − 1] = pu
+    KS_CHECK(sched_running_counts(s.schd(), s.sched_u.p, s.sched_u.p + k, (int)k, s.n_bind.p, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+int Engine::sched_deltas(int commit, std::vector<ks_sched_delta>* out, size_t* count, int64_t n_tasks,
+                         std::string& err) {
+    EngineImpl& s = *p_;
+    if (!s.solved) {
+        err = "no successful solve";
+        return KS_E_INVALID;
+    }
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    uint64_t* dense = nullptr;
+    size_t nt = 0;
+    int rc = scratch(&dense, std::max<int64_t>(n_tasks, 1), err);
+    if (rc == KS_OK) rc = task_pu(n_tasks ? dense : nullptr, n_tasks, &nt, n_tasks, err);   // also is_task / rank
+    if (rc) return rc;
+    const int64_t ncap = s.ncap;
+    if (!n_tasks) {   // no tasks: map arrays were not built; every binding is a preemption
+        KS_CHECK(s.map_is_task.ensure(ncap + 1));
+        KS_CHECK(s.map_rank.ensure(ncap + 1));
+        KS_CHECK(hipMemsetAsync(s.map_is_task.p, 0, (ncap + 1) * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.map_rank.p, 0, (ncap + 1) * sizeof(int), st));
+    }
+    KS_CHECK(s.sched_i.ensure(4 * (ncap + 1) + 4));
+    int* pre = s.sched_i.p;
+    int* other = pre + (ncap + 1);
+    int* pre_pos = other + (ncap + 1);
+    int* other_pos = pre_pos + (ncap + 1);
+    int* bad = other_pos + (ncap + 1);
+    KS_CHECK(hipMemsetAsync(bad, 0, 4 * sizeof(int), st));
+    const SchedDev d = s.schd();
+    KS_CHECK(sched_delta_kinds(d, s.map_is_task.p, s.map_rank.p, (const unsigned long long*)dense, pre, other, bad, st));
+    size_t t = 0;
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t, pre, pre_pos, (int)ncap + 1, st));
+    KS_CHECK(s.map_tmp.ensure(std::max(t, s.map_tmp.n)));
+    t = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, t, pre, pre_pos, (int)ncap + 1, st));
+    t = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, t, other, other_pos, (int)ncap + 1, st));
+    int h[3] = {0, 0, 0};
+    KS_CHECK(hipMemcpyAsync(&h[0], pre_pos + ncap, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipMemcpyAsync(&h[1], other_pos + ncap, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipMemcpyAsync(&h[2], bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    if (h[2]) {
+        err = "mapping names a destination that is not a PU (graph_manager.go:259-262)";
+        return KS_E_VERIFY;
+    }
+    const int npre = h[0], noth = h[1];
+    *count = (size_t)(npre + noth);
+    if (!out) return KS_OK;
+    KS_CHECK(s.sched_d.ensure(std::max(1, npre + noth)));
+    KS_CHECK(sched_delta_emit(d, s.map_rank.p, (const unsigned long long*)dense, pre, pre_pos, other, other_pos, npre,
+                              s.sched_d.p, commit, st));
+    out->resize(npre + noth);
+    if (npre + noth)
+        KS_CHECK(hipMemcpyAsync(out->data(), s.sched_d.p, (npre + noth) * sizeof(ks_sched_delta), hipMemcpyDeviceToHost,
+                                st));
+    KS_CHECK(hipStreamSynchronize(st));
+    return KS_OK;
+}
+
+int Engine::unsched_costs(const uint64_t* ids, size_t k, int mode, int64_t ucost, int64_t ccost, size_t* changed,
+                          std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    const int64_t nb = (s.nstore + 4) & ~3LL;   // byte flags, word-aligned for the atomics
+    KS_CHECK(s.sched_b.ensure(nb));
+    KS_CHECK(s.sched_i.ensure(4));
+    KS_CHECK(hipMemsetAsync(s.sched_b.p, 0, nb, st));
+    KS_CHECK(hipMemsetAsync(s.sched_i.p, 0, sizeof(int), st));
+    const unsigned long long* dids = nullptr;
+    if (ids && k) {
+        for (size_t i = 0; i < k; ++i)
+            if (ids[i] == 0 || (int64_t)ids[i] > s.nstore) {
+                err = "unscheduled aggregator id beyond the graph";
+                return KS_E_INVALID;
+            }
+        KS_CHECK(s.sched_u.ensure(k));
+        KS_CHECK(hipMemcpyAsync(s.sched_u.p, ids, k * 8, hipMemcpyHostToDevice, st));
+        dids = s.sched_u.p;
+    }
+    KS_CHECK(sched_unsched_costs(s.schd(), ids ? dids : nullptr, (int)k, s.sched_b.p, mode, ucost, ccost, s.sched_i.p,
+                                 st));
+    int h = 0;
+    KS_CHECK(hipMemcpyAsync(&h, s.sched_i.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    if (changed) *changed = (size_t)h;
+    if (h) s.solved = false;
+    return KS_OK;
+}
+
+int Engine::topology_stats(uint64_t mtpp, const uint64_t* pu_ids, const uint64_t* pu_running, size_t k,
+                           int64_t sink_slot, uint64_t* slots_below, uint64_t* running_below, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    if (!s.csr_valid) {   // the BFS walks the residual CSR's in-arcs
+        int rc = build(s, err);
+        if (rc) return rc;
+        s.has_prev = false;
+        s.solved = false;
+    }
+    const int64_t ncap = s.ncap, nn = s.nn;
+    if (sink_slot < 0 || sink_slot >= ncap || ncap == 0) {
+        std::memset(slots_below, 0, s.nslots * sizeof(uint64_t));
+        std::memset(running_below, 0, s.nslots * sizeof(uint64_t));
+        return KS_OK;
+    }
+    KS_CHECK(s.sched_u.ensure(3 * (ncap + 1) + 2 * k));
+    unsigned long long* cnt = s.sched_u.p;
+    unsigned long long* slots = cnt + (ncap + 1);
+    unsigned long long* run = slots + (ncap + 1);
+    unsigned long long* kid = run + (ncap + 1);
+    KS_CHECK(hipMemsetAsync(cnt, 0, 3 * (ncap + 1) * 8, st));
+    if (pu_ids && k) {
+        for (size_t i = 0; i < k; ++i)
+            if (pu_ids[i] == 0 || (int64_t)pu_ids[i] > ncap) {
+                err = "PU id beyond the graph";
+                return KS_E_INVALID;
+            }
+        KS_CHECK(hipMemcpyAsync(kid, pu_ids, k * 8, hipMemcpyHostToDevice, st));
+        KS_CHECK(hipMemcpyAsync(kid + k, pu_running, k * 8, hipMemcpyHostToDevice, st));
+    }
+    const SchedDev d = s.schd();
+    KS_CHECK(sched_running_counts(d, pu_ids ? kid : nullptr, kid + k, (int)k, cnt, st));
+    KS_CHECK(s.sched_i.ensure(3 * (nn + 1) + 2));
+    int* lvl = s.sched_i.p;
+    int* fa = lvl + (nn + 1);
+    int* fb = fa + (nn + 1);
+    int* nnext = fb + (nn + 1);
+    KS_CHECK(hipMemsetAsync(lvl, 0xff, (nn + 1) * sizeof(int), st));
+    int sink_x = 0;
+    KS_CHECK(hipMemcpyAsync(&sink_x, s.perm.p + sink_slot, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    const int zero = 0;
+    KS_CHECK(hipMemcpyAsync(lvl + sink_x, &zero, sizeof(int), hipMemcpyHostToDevice, st));
+    KS_CHECK(hipMemcpyAsync(fa, &sink_x, sizeof(int), hipMemcpyHostToDevice, st));
+    int nfront = 1;
+    for (int level = 0; nfront > 0 && level <= nn; ++level) {
+        KS_CHECK(hipMemsetAsync(nnext, 0, sizeof(int), st));
+        KS_CHECK(sched_topo_level(d, fa, nfront, level, lvl, fb, nnext, mtpp, cnt, slots, run, st));
+        KS_CHECK(hipMemcpyAsync(&nfront, nnext, sizeof(int), hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipStreamSynchronize(st));
+        std::swap(fa, fb);
+    }
+    const int64_t n = std::min<int64_t>(s.nslots, ncap);
+    if (n) {
+        KS_CHECK(hipMemcpyAsync(slots_below, slots, n * 8, hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipMemcpyAsync(running_below, run, n * 8, hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipStreamSynchronize(st));
+    }
     return KS_OK;
 }
 

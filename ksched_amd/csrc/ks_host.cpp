@@ -551,6 +551,77 @@ int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* coun
     return c->eng.task_pu(dev_out, cap, count, c->n_tasks, c->err);
 }
 
+int ks_set_bindings(ks_ctx* c, const uint64_t* task, const uint64_t* pu, size_t k) {
+    if (!c) return KS_E_INVALID;
+    if (k && (!task || !pu)) return c->fail(KS_E_INVALID, "null binding array");
+    for (size_t i = 0; i < k; ++i) {
+        if (!node_alive(c, task[i]) || c->nodes[task[i]].type != KS_NODE_TASK)
+            return c->fail(KS_E_INVALID, "binding of a node that is not a live task: " + std::to_string(task[i]));
+        if (pu[i] && (!node_alive(c, pu[i]) || c->nodes[pu[i]].type != KS_NODE_PU))
+            return c->fail(KS_E_INVALID, "binding to a node that is not a live PU: " + std::to_string(pu[i]));
+    }
+    return c->eng.set_bindings(task, pu, k, c->err);
+}
+
+int ks_scheduling_deltas(ks_ctx* c, int commit, ks_sched_delta* out, size_t cap, size_t* count) {
+    if (!c || !count) return KS_E_INVALID;
+    if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
+    size_t n = 0;
+    int rc = c->eng.sched_deltas(0, nullptr, &n, c->n_tasks, c->err);   // count (nothing committed)
+    if (rc || !out) {
+        *count = n;
+        return rc;
+    }
+    if (cap < n) {
+        *count = n;
+        return c->fail(KS_E_INVALID, "output buffer smaller than the delta count");
+    }
+    std::vector<ks_sched_delta> v;
+    rc = c->eng.sched_deltas(commit, &v, &n, c->n_tasks, c->err);
+    if (rc) return rc;
+    if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(ks_sched_delta));
+    *count = v.size();
+    return KS_OK;
+}
+
+int ks_update_unsched_costs(ks_ctx* c, const uint64_t* ids, size_t k, int32_t mode, int64_t unsched_cost,
+                            int64_t continuation_cost, size_t* changed) {
+    if (!c) return KS_E_INVALID;
+    if (mode != KS_COST_SET && mode != KS_COST_ADD) return c->fail(KS_E_INVALID, "unknown cost mode");
+    const int64_t lim = int64_t(1) << 40;
+    if (unsched_cost > lim || unsched_cost < -lim || continuation_cost > lim || continuation_cost < -lim)
+        return c->fail(KS_E_RANGE, "cost outside the supported range");
+    for (size_t i = 0; ids && i < k; ++i)
+        if (!node_alive(c, ids[i])) return c->fail(KS_E_INVALID, "unscheduled aggregator " + std::to_string(ids[i]) +
+                                                                     " is not a live node");
+    size_t ch = 0;
+    int rc = c->eng.unsched_costs(ids, ids ? k : 0, mode, unsched_cost, continuation_cost, &ch, c->err);
+    if (rc == KS_OK && ch) {
+        c->have_solution = false;
+        c->flows_fresh = false;
+    }
+    if (changed) *changed = ch;
+    return rc;
+}
+
+int ks_topology_stats(ks_ctx* c, uint64_t max_tasks_per_pu, const uint64_t* pu_ids, const uint64_t* pu_running,
+                      size_t k, uint64_t* slots_below, uint64_t* running_below, size_t cap, size_t* count) {
+    if (!c || !count) return KS_E_INVALID;
+    const size_t n = (size_t)c->nslots();
+    *count = n;
+    if (!slots_below || !running_below) return KS_OK;
+    if (cap < n) return c->fail(KS_E_INVALID, "output buffers smaller than the node id range");
+    if (pu_ids && k && !pu_running) return c->fail(KS_E_INVALID, "null running-count array");
+    for (size_t i = 0; pu_ids && i < k; ++i)
+        if (!node_alive(c, pu_ids[i]) || c->nodes[pu_ids[i]].type != KS_NODE_PU)
+            return c->fail(KS_E_INVALID, "running count for a node that is not a live PU");
+    const int64_t sink = c->n_sinks == 1 ? (int64_t)c->sink_id - 1 : -1;
+    int rc = c->eng.topology_stats(max_tasks_per_pu, pu_ids, pu_running, pu_ids ? k : 0, sink, slots_below,
+                                   running_below, c->err);
+    if (!c->eng.solved()) c->have_solution = c->flows_fresh = false;   // a pending CSR rebuild ran
+    return rc;
+}
+
 int ks_get_store_stats(ks_ctx* c, ks_store_stats* out) {
     if (!c || !out) return KS_E_INVALID;
     c->eng.store_stats(out);

@@ -61,6 +61,8 @@ struct StoreDev {
     unsigned char* n_alive;
     unsigned char* n_fresh;       // per slot: (re)created since the last solve (warm start)
     int* n_lastrm;                // per slot: last REMOVE position of the current apply, −1
+    unsigned char* n_grow;        // per slot: an insert did not fit its segment (next build doubles it)
+    unsigned long long* n_bind;   // per slot: bound PU node id (task bindings), 0 = none
     const int* perm;              // slot → internal id
     // arc table, by slot
     int acap;
@@ -69,6 +71,7 @@ struct StoreDev {
     long long* a_low;
     long long* a_cap;
     long long* a_cost;
+    unsigned char* a_type;        // flowgraph.ArcType (1 = running)
     unsigned char* a_alive;
     int* fwd;                     // forward residual position, −1 = none
     int* free_stack;

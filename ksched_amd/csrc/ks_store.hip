@@ -177,6 +177,7 @@ __global__ void k_node_edits(StoreDev d, const NodeEdit* __restrict__ e, int ne)
         d.n_alive[x.slot] = x.alive;
         d.n_type[x.slot] = x.type;
         if (x.alive && (x.last_rm >= 0 || !x.was_alive)) d.n_fresh[x.slot] = 1;
+        if (x.last_rm >= 0 || !x.alive) d.n_bind[x.slot] = 0;   // a removed task is unbound (scheduler.go:106-132)
     }
 }
 
@@ -235,6 +236,7 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
         d.a_low[s] = low;
         d.a_cap[s] = cap;
         d.a_cost[s] = x.cost;
+        d.a_type[s] = (unsigned char)(x.type < 0 ? 0 : (x.type > 255 ? 255 : x.type));
         if (!d.csr_valid) continue;
         const int xs = perm_of(d, sl), xd = perm_of(d, dl);
         if (xs < 0 || xd < 0) {
@@ -264,6 +266,8 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
         const int p = d.first[xs] + ps, q = d.first[xd] + pd;
         if (p >= d.first[xs + 1] || q >= d.first[xd + 1]) {
             d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
+            if (p >= d.first[xs + 1]) d.n_grow[sl] = 1;
+            if (q >= d.first[xd + 1]) d.n_grow[dl] = 1;
             continue;
         }
         d.head[p] = xd;

@@ -19,8 +19,11 @@ KS_ADD_NODE, KS_REMOVE_NODE, KS_ADD_ARC, KS_UPDATE_ARC, KS_SET_EXCESS = 0, 1, 2,
 EXPORTED_SYMBOLS = (
     "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
     "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
-    "ks_coalesce_deltas", "ks_get_store_stats",
+    "ks_coalesce_deltas", "ks_get_store_stats", "ks_set_bindings", "ks_scheduling_deltas",
+    "ks_update_unsched_costs", "ks_topology_stats",
 )
+KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
+KS_COST_SET, KS_COST_ADD = 0, 1
 
 NODE_DT = np.dtype({"names": ["id", "excess", "type", "_pad"],
                     "formats": ["<u8", "<i8", "<i4", "<i4"], "offsets": [0, 8, 16, 20], "itemsize": 24})
@@ -30,6 +33,8 @@ ARC_DT = np.dtype({"names": ["src", "dst", "low", "cap", "cost", "type", "_pad"]
 DELTA_DT = np.dtype({"names": ["kind", "type", "id", "src", "dst", "low", "cap", "cost", "old_cost", "excess"],
                      "formats": ["<i4", "<i4", "<u8", "<u8", "<u8", "<u8", "<u8", "<i8", "<i8", "<i8"],
                      "offsets": [0, 4, 8, 16, 24, 32, 40, 48, 56, 64], "itemsize": 72})
+SCHED_DELTA_DT = np.dtype({"names": ["type", "_pad", "task", "pu"], "formats": ["<i4", "<i4", "<u8", "<u8"],
+                           "offsets": [0, 4, 8, 16], "itemsize": 24})
 FLOW_DT = np.dtype({"names": ["src", "dst", "flow"], "formats": ["<u8", "<u8", "<i8"],
                     "offsets": [0, 8, 16], "itemsize": 24})
 
@@ -118,6 +123,10 @@ def load(build_if_missing: bool = True):
     L.ks_solve_many.argtypes = [P(V), C.c_size_t, C.c_int, P(KsResult)]
     L.ks_coalesce_deltas.argtypes = [V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_store_stats.argtypes = [V, P(KsStoreStats)]
+    L.ks_set_bindings.argtypes = [V, V, V, C.c_size_t]
+    L.ks_scheduling_deltas.argtypes = [V, C.c_int, V, C.c_size_t, P(C.c_size_t)]
+    L.ks_update_unsched_costs.argtypes = [V, V, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_size_t)]
+    L.ks_topology_stats.argtypes = [V, C.c_uint64, V, V, C.c_size_t, V, V, C.c_size_t, P(C.c_size_t)]
     _LIB = L
     return L
 
@@ -218,6 +227,47 @@ class Context:
         st = KsStoreStats()
         self._check(self._L.ks_get_store_stats(self._h, C.byref(st)))
         return st.as_dict()
+
+    # -- scheduler-side sweeps on device (ks_sched.hip) ----------------------
+    def set_bindings(self, bindings: dict[int, int]):
+        t = np.fromiter(bindings.keys(), np.uint64, len(bindings))
+        p = np.fromiter(bindings.values(), np.uint64, len(bindings))
+        self._check(self._L.ks_set_bindings(self._h, t.ctypes.data, p.ctypes.data, t.shape[0]))
+
+    def scheduling_deltas(self, commit: bool = True) -> np.ndarray:
+        """PREEMPT / PLACE / MIGRATE records (SCHED_DELTA_DT) of the last solve."""
+        cnt = C.c_size_t()
+        self._check(self._L.ks_scheduling_deltas(self._h, 0, None, 0, C.byref(cnt)))
+        out = np.zeros(cnt.value, SCHED_DELTA_DT)
+        self._check(self._L.ks_scheduling_deltas(self._h, int(commit), out.ctypes.data, cnt.value, C.byref(cnt)))
+        return out[:cnt.value]
+
+    def update_unsched_costs(self, cost: int, mode: int = KS_COST_SET, continuation: int = 0,
+                             unsched_ids=None) -> int:
+        ch = C.c_size_t()
+        ids = None if unsched_ids is None else np.ascontiguousarray(unsched_ids, np.uint64)
+        self._check(self._L.ks_update_unsched_costs(self._h, None if ids is None else ids.ctypes.data,
+                                                    0 if ids is None else ids.shape[0], mode, cost, continuation,
+                                                    C.byref(ch)))
+        return ch.value
+
+    def topology_stats(self, max_tasks_per_pu: int, pu_running: dict[int, int] | None = None):
+        """(slots_below, running_below) per node id − 1."""
+        cnt = C.c_size_t()
+        self._check(self._L.ks_topology_stats(self._h, max_tasks_per_pu, None, None, 0, None, None, 0,
+                                              C.byref(cnt)))
+        sl = np.zeros(cnt.value, np.uint64)
+        rn = np.zeros(cnt.value, np.uint64)
+        ids = vals = None
+        k = 0
+        if pu_running is not None:
+            ids = np.fromiter(pu_running.keys(), np.uint64, len(pu_running))
+            vals = np.fromiter(pu_running.values(), np.uint64, len(pu_running))
+            k = ids.shape[0]
+        self._check(self._L.ks_topology_stats(self._h, max_tasks_per_pu, None if ids is None else ids.ctypes.data,
+                                              None if vals is None else vals.ctypes.data, k, sl.ctypes.data,
+                                              rn.ctypes.data, cnt.value, C.byref(cnt)))
+        return sl, rn
 
     def task_pu_device(self, dev_ptr: int, cap: int) -> int:
         cnt = C.c_size_t()

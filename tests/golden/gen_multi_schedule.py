@@ -481,6 +481,9 @@ class Scheduler:                                 # flowscheduler/scheduler.go
         if not jds:
             return 0, None
         self.gm.compute_topology_statistics()
+        self.stats = {"pu_running": {str(n.id): len(n.rd.current_running) for n in self.gm.res_node.values()
+                                     if n.type == PU},
+                      "slots_running": {str(n.id): [n.rd.slots, n.rd.running] for n in self.gm.res_node.values()}}
         self.gm.add_or_update_job_nodes(jds)
         mapping, info = solve(self.gm)
         # SchedulingDeltasForPreemptedTasks (:297-339): no task is preempted here; clear lists
@@ -513,7 +516,13 @@ class Scheduler:                                 # flowscheduler/scheduler.go
             td.state = RUNNING
             placed += 1
         info["placed"] = placed
+        info["topology_stats"] = self.stats      # ComputeTopologyStatistics at the round's start
+        info["deltas"] = [[kind, self._node_of_task(tid), self.gm.res_node[rd.uuid].id] for kind, tid, rd in deltas]
         return placed, info
+
+    def _node_of_task(self, tid):
+        n = self.gm.task_node.get(tid)
+        return n.id if n is not None else 0
 
     def complete(self, td):                      # HandleTaskCompletion (:106-132)
         del self.bindings[td.uid]

@@ -79,3 +79,21 @@ def test_daemon_parses_the_stream(coalesce):
     assert p.returncode == 0, p.stderr
     lines = p.stdout.splitlines()
     assert len(lines) == 5 and lines[0].startswith("iteration full nodes 15 arcs 19")
+
+
+def test_restatements_reproduce_the_reference_trace():
+    """oracle/sched_ref.py (the checker of the device sweeps) against the
+    reference simulation: per round, ComputeTopologyStatistics on the replayed
+    graph and the scheduling deltas of the recorded mapping."""
+    from oracle import sched_ref
+    bindings = {}
+    for r, g in replay_graphs():
+        ts = r["topology_stats"]
+        res = set(int(k) for k in ts["slots_running"])
+        got = sched_ref.topology_stats(g, res, {int(k): v for k, v in ts["pu_running"].items()}, 1)
+        assert got == {int(k): tuple(v) for k, v in ts["slots_running"].items()}, r["round"]
+        mp = {int(k): v for k, v in r["mapping"].items()}
+        live = (np.nonzero(g.ntype == 1)[0] + 1).tolist()      # completed tasks are unbound (scheduler.go:106-132)
+        d = sched_ref.scheduling_deltas(bindings, mp, live)
+        assert [(k, t, p) for k, t, p in d] == [(sched_ref.PLACE, t, p) for _, t, p in r["deltas"]]
+        bindings = sched_ref.apply_deltas(bindings, d)
