@@ -227,6 +227,11 @@ int ks_get_task_mapping(ks_ctx* ctx, uint64_t* task, uint64_t* pu,
  * *count, the number of task nodes. */
 int ks_get_task_pu_device(ks_ctx* ctx, uint64_t* dev_out, size_t cap, size_t* count);
 
+/* The device-resident graph as it stands (the reference's dimacs.Export view,
+ * export.go:11-29, e.g. for a checkpoint or a DIMACS dump): live nodes in id order
+ * and live arcs in arc-slot order. Call with caps of 0 to size. */
+int ks_get_graph(ks_ctx* ctx, ks_node* nodes, size_t ncap, size_t* n, ks_arc* arcs, size_t acap, size_t* m);
+
 /* Store counters (no device work). */
 int ks_get_store_stats(ks_ctx* ctx, ks_store_stats* out);
 

@@ -191,6 +191,7 @@ class Cell:
             self.state[sl] = self.DEAD
 
         # 3. arrivals (FIFO id reuse, then fresh ids)
+        arrived = []
         if arrive:
             x = gen.stream(seed, 1 << 32, 9 * arrive).reshape(arrive, 9)
             J, R = self.J, self.R
@@ -214,6 +215,7 @@ class Cell:
                     self._grow(self.n_slots + 1)
                     self.n_slots += 1
                 si = ti - self.TASK0
+                arrived.append(si)
                 self.state[si] = self.WAIT
                 self.job[si] = j[a]
                 self.adst[si] = dsts[a]
@@ -222,10 +224,14 @@ class Cell:
                 for d, c in zip(dsts[a].tolist(), costs[a].tolist()):
                     out.append((KS_ADD_ARC, 0, 0, ti, d, 0, 1, c, 0, 0))
 
-        # 4. ageing of the tasks that were already waiting
+        # 4. ageing of the tasks that were already waiting (not an arrival that took
+        #    over the id of a task that completed this round)
         if age_cost:
             ns0 = waiting_before.shape[0]
-            aged = np.nonzero(waiting_before & (self.state[:ns0] == self.WAIT))[0]
+            still = waiting_before & (self.state[:ns0] == self.WAIT)
+            fresh = np.asarray([a for a in arrived if a < ns0], np.int64)
+            still[fresh] = False
+            aged = np.nonzero(still)[0]
             for si in aged.tolist():
                 c = int(self.acost[si, 0])
                 ti = self.TASK0 + si

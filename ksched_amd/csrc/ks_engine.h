@@ -45,6 +45,9 @@ public:
     // place (the previous solve's, edited by the deltas since).
     int solve(ks_result& r, bool warm, std::string& err);
 
+    // Live arcs of the store (1-based ids), arc-slot order.
+    int arcs(std::vector<ks_arc>& out, std::string& err);
+
     // Arcs with positive flow in the last solve (the "f" lines), arc-slot order.
     int flows(std::vector<ks_flow>& out, std::string& err);
 

@@ -1662,6 +1662,29 @@ __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, con
     }
 }
 
+struct SlotAlive {
+    const unsigned char* alive;
+    __host__ __device__ bool operator()(const int& s) const { return alive[s] != 0; }
+};
+
+__global__ void k_arc_records(int cnt, const int* __restrict__ sel, const int* __restrict__ src,
+                              const int* __restrict__ dst, const long long* __restrict__ low,
+                              const long long* __restrict__ cap, const long long* __restrict__ cost,
+                              const unsigned char* __restrict__ type, ks_arc* __restrict__ out) {
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < cnt; i += (long long)gridDim.x * BLK) {
+        const int s = sel[i];
+        ks_arc a;
+        a.src = (uint64_t)src[s] + 1;
+        a.dst = (uint64_t)dst[s] + 1;
+        a.low = (uint64_t)low[s];
+        a.cap = (uint64_t)cap[s];
+        a.cost = cost[s];
+        a.type = type[s];
+        a._pad = 0;
+        out[i] = a;
+    }
+}
+
 // positive-flow arcs of the last solve as "f" records (ks_flow), slot order
 struct FlowPositive {
     const unsigned char* alive;
@@ -2661,6 +2684,39 @@ int Engine::topology_stats(uint64_t mtpp, const uint64_t* pu_ids, const uint64_t
         KS_CHECK(hipMemcpyAsync(running_below, run, n * 8, hipMemcpyDeviceToHost, st));
         KS_CHECK(hipStreamSynchronize(st));
     }
+    return KS_OK;
+}
+
+int Engine::arcs(std::vector<ks_arc>& out, std::string& err) {
+    EngineImpl& s = *p_;
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    const int hi = s.hi();
+    out.clear();
+    if (!hi) return KS_OK;
+    KS_CHECK(s.flow_sel.ensure(hi));
+    KS_CHECK(s.flow_cnt.ensure(1));
+    hipcub::CountingInputIterator<int> it(0);
+    SlotAlive pred{s.a_alive.p};
+    size_t t = 0;
+    KS_CHECK(hipcub::DeviceSelect::If(nullptr, t, it, s.flow_sel.p, s.flow_cnt.p, hi, pred, st));
+    KS_CHECK(s.map_tmp.ensure(std::max(t, s.map_tmp.n)));
+    t = s.map_tmp.n;
+    KS_CHECK(hipcub::DeviceSelect::If(s.map_tmp.p, t, it, s.flow_sel.p, s.flow_cnt.p, hi, pred, st));
+    int cnt = 0;
+    KS_CHECK(hipMemcpyAsync(&cnt, s.flow_cnt.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    if (!cnt) return KS_OK;
+    ks_arc* d = nullptr;
+    KS_CHECK(hipMalloc(&d, cnt * sizeof(ks_arc)));
+    hipLaunchKernelGGL(k_arc_records, dim3(grid_for(cnt)), dim3(BLK), 0, st, cnt, (const int*)s.flow_sel.p,
+                       (const int*)s.a_src.p, (const int*)s.a_dst.p, (const long long*)s.a_low.p,
+                       (const long long*)s.a_cap.p, (const long long*)s.a_cost.p, (const unsigned char*)s.a_type.p, d);
+    out.resize(cnt);
+    hipError_t e = hipMemcpyAsync(out.data(), d, cnt * sizeof(ks_arc), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    KS_CHECK(e);
     return KS_OK;
 }
 

@@ -622,6 +622,24 @@ int ks_topology_stats(ks_ctx* c, uint64_t max_tasks_per_pu, const uint64_t* pu_i
     return rc;
 }
 
+int ks_get_graph(ks_ctx* c, ks_node* nodes, size_t ncap, size_t* n, ks_arc* arcs, size_t acap, size_t* m) {
+    if (!c || !n || !m) return KS_E_INVALID;
+    size_t k = 0;
+    for (uint64_t id = 1; id < c->nodes.size(); ++id) {
+        const NodeRec& r = c->nodes[id];
+        if (!r.alive) continue;
+        if (nodes && k < ncap) nodes[k] = ks_node{id, r.excess, r.type, 0};
+        ++k;
+    }
+    *n = k;
+    std::vector<ks_arc> v;
+    int rc = c->eng.arcs(v, c->err);
+    if (rc) return rc;
+    if (arcs) std::memcpy(arcs, v.data(), std::min(acap, v.size()) * sizeof(ks_arc));
+    *m = v.size();
+    return KS_OK;
+}
+
 int ks_get_store_stats(ks_ctx* c, ks_store_stats* out) {
     if (!c || !out) return KS_E_INVALID;
     c->eng.store_stats(out);

@@ -20,7 +20,7 @@ EXPORTED_SYMBOLS = (
     "ks_abi_version", "ks_default_opts", "ks_create", "ks_destroy", "ks_last_error", "ks_load_graph",
     "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
     "ks_coalesce_deltas", "ks_get_store_stats", "ks_set_bindings", "ks_scheduling_deltas",
-    "ks_update_unsched_costs", "ks_topology_stats",
+    "ks_update_unsched_costs", "ks_topology_stats", "ks_get_graph",
 )
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
@@ -123,6 +123,7 @@ def load(build_if_missing: bool = True):
     L.ks_solve_many.argtypes = [P(V), C.c_size_t, C.c_int, P(KsResult)]
     L.ks_coalesce_deltas.argtypes = [V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_store_stats.argtypes = [V, P(KsStoreStats)]
+    L.ks_get_graph.argtypes = [V, V, C.c_size_t, P(C.c_size_t), V, C.c_size_t, P(C.c_size_t)]
     L.ks_set_bindings.argtypes = [V, V, V, C.c_size_t]
     L.ks_scheduling_deltas.argtypes = [V, C.c_int, V, C.c_size_t, P(C.c_size_t)]
     L.ks_update_unsched_costs.argtypes = [V, V, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_size_t)]
@@ -227,6 +228,16 @@ class Context:
         st = KsStoreStats()
         self._check(self._L.ks_get_store_stats(self._h, C.byref(st)))
         return st.as_dict()
+
+    def graph(self):
+        """The device-resident graph: (nodes NODE_DT, arcs ARC_DT)."""
+        n, m = C.c_size_t(), C.c_size_t()
+        self._check(self._L.ks_get_graph(self._h, None, 0, C.byref(n), None, 0, C.byref(m)))
+        nodes = np.zeros(n.value, NODE_DT)
+        arcs = np.zeros(m.value, ARC_DT)
+        self._check(self._L.ks_get_graph(self._h, nodes.ctypes.data, n.value, C.byref(n), arcs.ctypes.data, m.value,
+                                         C.byref(m)))
+        return nodes, arcs
 
     # -- scheduler-side sweeps on device (ks_sched.hip) ----------------------
     def set_bindings(self, bindings: dict[int, int]):

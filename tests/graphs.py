@@ -177,3 +177,16 @@ def load_multi_schedule():
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multi_schedule_iteration.json")
     with open(p) as f:
         return json.load(f)["rounds"]
+
+
+def same_graph(ctx, g):
+    """The device-resident graph (ks_get_graph) equals g up to arcs of capacity 0
+    (an "x … 0 0" record removes them from the store)."""
+    nodes, arcs = ctx.graph()
+    dev = sorted(zip(arcs["src"].tolist(), arcs["dst"].tolist(), arcs["low"].tolist(), arcs["cap"].tolist(),
+                     arcs["cost"].tolist()))
+    want = sorted(a for a in zip(g.src.tolist(), g.dst.tolist(), g.low.tolist(), g.cap.tolist(), g.cost.tolist())
+                  if a[3] > 0)
+    assert dev == want
+    live = np.nonzero(g.ntype != 0)[0] + 1
+    assert set(live.tolist()) <= set(nodes["id"].tolist())

@@ -4,6 +4,7 @@ cost and flow against the CPU oracle on the equivalent full graphs."""
 import numpy as np
 import pytest
 
+from graphs import same_graph
 from test_gpu_parity import check_mapping, flows_by_arc
 from ksched_amd import churn, gen, native
 from oracle import ko
@@ -209,6 +210,7 @@ def test_deltas_applied_in_place_on_device():
             r = ctx.solve()
             rebuilt.append(r.raw["rebuilt"])
             g = cell.graph()
+            same_graph(ctx, g)                     # ks_get_graph: the store equals the reference graph
             # "x … 0 0" capacity refreshes delete arcs the full graph keeps at capacity 0
             assert st["live_arcs"] == r.raw["n_arcs"] == int((g.cap > 0).sum())
             cst, cost, flow, _ = ko.cost_scaling(g)

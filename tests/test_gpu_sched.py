@@ -6,7 +6,7 @@ scheduling deltas (graph_manager.go:253-339), ComputeTopologyStatistics
 import numpy as np
 import pytest
 
-from graphs import graph_from_lists, load_multi_schedule, parse_dimacs
+from graphs import graph_from_lists, load_multi_schedule, parse_dimacs, same_graph
 from ksched_amd import churn, gen, native
 from oracle import ko, sched_ref
 
@@ -86,7 +86,8 @@ def test_topology_statistics_config3_size():
     rng = np.random.default_rng(5)
     pus = (np.nonzero(g.ntype == 2)[0] + 1).tolist()
     running = {p: int(x) for p, x in zip(pus, rng.integers(0, 4, len(pus)))}
-    resource = set((np.nonzero(np.isin(g.ntype, [2, 4, 5]))[0] + 1).tolist()) | {2}
+    # resources: PUs, machines, the racks and X (type 0 here, like ksched's coordinator)
+    resource = set((np.nonzero(np.isin(g.ntype, [2, 4, 5]))[0] + 1).tolist()) | set(range(2, 3 + R))
     want = sched_ref.topology_stats(g, resource, running, 10)
     with native.Context(0) as ctx:
         ctx.load_graph(g)
@@ -115,6 +116,7 @@ def test_unscheduled_cost_ageing_on_device_matches_the_stream():
             assert changed == waiting                # every task waiting before the round
             a.apply_deltas(da)
             b.apply_deltas(db)
+            same_graph(b, cell_a.graph())
             ra, rb = a.solve(), b.solve()
             st, cost, flow, _ = ko.cost_scaling(cell_a.graph())
             assert st == 0 and ra.cost == cost and rb.cost == cost
