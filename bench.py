@@ -72,6 +72,39 @@ def roofline_of(results):
                                             "bytes": bf_b}}}
 
 
+def timed_cpu(fn, reps: int = 5, warmup: int = 1, pin: bool = True):
+    """BASELINE.md §3-4 protocol for a CPU baseline: `warmup` untimed runs, then the
+    median of `reps` timed runs, the calling thread pinned to one core (taskset-like,
+    os.sched_setaffinity) when `pin`. → (median seconds, all times, last result, core)."""
+    core = None
+    old = None
+    if pin and hasattr(os, "sched_setaffinity"):
+        old = os.sched_getaffinity(0)
+        core = min(old)
+        os.sched_setaffinity(0, {core})
+    try:
+        out = None
+        for _ in range(warmup):
+            out = fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = fn()
+            ts.append(time.perf_counter() - t0)
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
+    return float(np.median(ts)), ts, out, core
+
+
+def host_cores() -> int:
+    """Cores this process may use (the GPU box exposes the whole machine's CPUs but
+    grants a share: OMP_NUM_THREADS is set to it there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(env))) if env and env.isdigit() else n
+
+
 class Dist:
     """torch.distributed over RCCL when launched with WORLD_SIZE > 1.
 
@@ -149,14 +182,25 @@ def run_full(args, D):
     g = gen.quincy(T, M, R, J, seed + D.rank)
     ctx = native.Context(D.local, **full_opts(args))
     ctx.load_graph(g)
+    import torch
+    dev_map = torch.zeros(T, dtype=torch.int64, device=f"cuda:{D.local}") if torch.cuda.is_available() else None
+
+    def step():
+        # Solve() → TaskMapping (placement/solver.go:60-90, 183-269): the device solve
+        # and the device-side decomposition into the task→PU vector (stays in HBM)
+        r = ctx.solve()
+        if dev_map is not None:
+            ctx.task_pu_device(dev_map.data_ptr(), T)
+        return r
+
     for _ in range(args.warmup):
-        ctx.solve()
+        step()
     D.sync()
     t0 = time.perf_counter()
     results, step_ms = [], []
     for _ in range(args.steps):
         ts = time.perf_counter()
-        results.append(ctx.solve())
+        results.append(step())
         step_ms.append(1e3 * (time.perf_counter() - ts))
     D.sync()
     elapsed = D.max(time.perf_counter() - t0)
@@ -165,10 +209,8 @@ def run_full(args, D):
 
     gather = None
     if D.dist:       # RCCL gather of the task→PU mappings (int64 PU id per task, 0 = unscheduled)
-        torch = D.torch
-        buf = torch.zeros(1, T, dtype=torch.int64, device="cuda")
+        buf = dev_map.view(1, T)
         tg0 = time.perf_counter()
-        ctx.task_pu_device(buf.data_ptr(), T)
         out = D.gather(buf, D.world)
         torch.cuda.synchronize()
         gather = {"ms": 1e3 * (time.perf_counter() - tg0), "bytes_per_rank": T * 8,
@@ -179,23 +221,23 @@ def run_full(args, D):
     parity = {"gpu_costs": costs, "flow": results[-1].flow}
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from oracle import ko
-        t1 = time.perf_counter()
-        st, ccost, cflow, nmap, ms = ko.reference_path(g)
-        dt = time.perf_counter() - t1
-        t2 = time.perf_counter()
-        st2, cs_cost, cs_flow, _ = ko.cost_scaling(g)
-        dt2 = time.perf_counter() - t2
-        cpu = {"value": round(g.m / dt, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
-               "sample": f"one full reference-path solve of the same {args.config} graph "
-                         f"(DIMACS export -> successive shortest path -> f lines -> BFS mapping), "
-                         f"{dt:.1f} s single-threaded",
-               "ms": round(1e3 * dt, 1), "phases_ms": [round(x, 1) for x in ms],
-               "strong_cpu_cost_scaling": {"value": round(g.m / dt2, 1), "unit": "arcs/s", "ms": round(1e3 * dt2, 1),
-                                           "cores": 1}}
+        med, ts, out, core = timed_cpu(lambda: ko.reference_path(g), reps=args.cpu_reps)
+        st, ccost, cflow, nmap, ms = out
+        med2, ts2, out2, _ = timed_cpu(lambda: ko.cost_scaling(g), reps=args.cpu_reps)
+        st2, cs_cost, cs_flow, _ = out2
+        cpu = {"value": round(g.m / med, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
+               "sample": f"the same {args.config} graph through the in-repo restatement of the reference CPU path "
+                         f"(DIMACS export -> successive shortest path -> f lines -> BFS mapping), median of "
+                         f"{len(ts)} after 1 warm-up, pinned to core {core}",
+               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts),
+               "pinned_core": core, "phases_ms": [round(x, 1) for x in ms],
+               "strong_cpu_cost_scaling": {"value": round(g.m / med2, 1), "unit": "arcs/s", "ms": round(1e3 * med2, 1),
+                                           "median_of": len(ts2), "cores": 1}}
         parity.update({"cpu_cost": ccost, "cpu_flow": cflow, "cs_cost": cs_cost,
                        "match": costs == [ccost] == [cs_cost] and results[-1].flow == cflow})
     config = {"workload": f"{args.config}: Quincy-shaped cell graph T={T} M={M} R={R} J={J} "
-                          f"(n={g.n}, m={g.m}), full device re-solve per step, one graph per GPU",
+                          f"(n={g.n}, m={g.m}), step = full device re-solve + device task->PU extraction "
+                          f"(Solve() -> TaskMapping), one graph per GPU",
               "tasks": T, "machines": M, "racks": R, "jobs": J, "seed": seed, "n": g.n, "m": g.m,
               "parallelism": f"independent graphs x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
@@ -250,12 +292,13 @@ def run_incremental(args, D):
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from oracle import ko
         g = cell.graph()
-        t1 = time.perf_counter()
-        st, ccost, cflow, _, ms = ko.reference_path(g)
-        dt = time.perf_counter() - t1
-        cpu = {"value": round(g.m / dt, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
-               "sample": f"one reference-path solve (export -> SSP -> f lines -> BFS) of the last round's "
-                         f"full graph, {dt:.1f} s single-threaded", "ms": round(1e3 * dt, 1)}
+        med, ts, out, core = timed_cpu(lambda: ko.reference_path(g), reps=args.cpu_reps)
+        st, ccost, cflow, _, ms = out
+        cpu = {"value": round(g.m / med, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
+               "sample": f"the last round's full graph through the restatement of the reference CPU path (export "
+                         f"-> SSP -> f lines -> BFS), median of {len(ts)} after 1 warm-up, pinned to core {core}",
+               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts),
+               "pinned_core": core}
         parity = {"last_round_gpu_cost": rounds[-1]["cost"], "cpu_cost": ccost, "cpu_flow": cflow,
                   "match": rounds[-1]["cost"] == ccost and rounds[-1]["flow"] == cflow}
     config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
@@ -273,13 +316,29 @@ def run_batch(args, D):
     T, M, R, J, _ = gen.CONFIGS["config2"]
     num = args.graphs
     mine = batch.assign(num, D.world, D.rank)
-    graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in mine]
-    if args.batch_mode == "union":
+    if D.rehearsal and args.batch_mode == "abi":
+        args.batch_mode = "union"    # both ranks on GPU 0: RCCL refuses two ranks per device
+    if args.batch_mode == "abi":
+        # the C-ABI batch (ks_batch_*): every rank passes all graphs, owns g ≡ rank (mod world),
+        # solves the union of its graphs; per-graph rows to rank 0 over RCCL inside libksmcmf
+        all_graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in range(num)]
+        graphs = [all_graphs[k] for k in mine]
+        if D.world > 1:
+            uid = [native.Batch.unique_id() if D.rank == 0 else None]
+            D.dist.broadcast_object_list(uid, src=0)
+            bt = native.Batch(device=D.local, world=D.world, rank=D.rank, uid=uid[0], **full_opts(args))
+        else:
+            bt = native.Batch(devices=[D.local], **full_opts(args))
+        bt.load(all_graphs)
+        solve = bt.solve
+    elif args.batch_mode == "union":
+        graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in mine]
         u, noff, _ = batch.union(graphs)
         ctxs = [native.Context(D.local, **full_opts(args))]
         ctxs[0].load_graph(u)
         solve = lambda: [ctxs[0].solve()]
     else:
+        graphs = [gen.quincy(T, M, R, J, 1000 + k) for k in mine]
         ctxs = [native.Context(D.local, **full_opts(args)) for _ in graphs]
         for c, g in zip(ctxs, graphs):
             c.load_graph(g)
@@ -300,50 +359,63 @@ def run_batch(args, D):
     arcs_all = num * gen.quincy_sizes(T, M, R, J)[1]
     value = arcs_all / (ms_per_step / 1e3)
 
-    # task→PU mappings: device-resident [slots, T] block per rank (PU id local to its
-    # cell, 0 = unscheduled), all-gathered over RCCL after the timed region
+    # after the timed region: per-graph cost/flow and task→PU rows gathered to rank 0
     gather = None
-    import torch
-    if torch.cuda.is_available():
-        slots = batch.slots_per_rank(num, D.world)
-        buf = torch.zeros(slots, T, dtype=torch.int64, device=f"cuda:{D.local}")
+    per_graph = None
+    if args.batch_mode == "abi":
         tg0 = time.perf_counter()
-        if args.batch_mode == "union":
-            ctxs[0].task_pu_device(buf.data_ptr(), len(mine) * T)
-            off = torch.as_tensor(noff[:len(mine)], device=buf.device).view(-1, 1)
-            part = buf[:len(mine)]
-            part.sub_(torch.where(part > 0, off, torch.zeros_like(off)))
-        else:
-            for i, c in enumerate(ctxs):
-                c.task_pu_device(buf[i].data_ptr(), T)
-        full = D.gather(buf, num) if D.dist else buf[:num]
-        torch.cuda.synchronize()
-        gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
-                  "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
-
-    if args.batch_mode == "union":
-        per_graph = batch.split_costs(u, noff, ctxs[0].flows())
+        pu, cost, flow = bt.gather(T, root=D.rank == 0)
+        gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "via": "RCCL ncclSend/ncclRecv in libksmcmf",
+                  "bytes_per_rank": batch.slots_per_rank(num, D.world) * (T + 2) * 8}
+        if D.rank == 0:
+            per_graph = cost
+            gather.update({"graphs": int(pu.shape[0]), "scheduled": int((pu > 0).sum()),
+                           "flow_total": int(flow.sum())})
     else:
-        per_graph = np.asarray([r.cost for r in results[-len(ctxs):]], np.int64)
+        import torch
+        if torch.cuda.is_available():
+            slots = batch.slots_per_rank(num, D.world)
+            buf = torch.zeros(slots, T, dtype=torch.int64, device=f"cuda:{D.local}")
+            tg0 = time.perf_counter()
+            if args.batch_mode == "union":
+                ctxs[0].task_pu_device(buf.data_ptr(), len(mine) * T)
+                off = torch.as_tensor(noff[:len(mine)], device=buf.device).view(-1, 1)
+                part = buf[:len(mine)]
+                part.sub_(torch.where(part > 0, off, torch.zeros_like(off)))
+            else:
+                for i, c in enumerate(ctxs):
+                    c.task_pu_device(buf[i].data_ptr(), T)
+            full = D.gather(buf, num) if D.dist else buf[:num]
+            torch.cuda.synchronize()
+            gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "bytes_per_rank": slots * T * 8,
+                      "graphs": int(full.shape[0]), "scheduled": int((full > 0).sum().item())}
+        if args.batch_mode == "union":
+            per_graph = batch.split_costs(u, noff, ctxs[0].flows())
+        else:
+            per_graph = np.asarray([r.cost for r in results[-len(ctxs):]], np.int64)
     cpu = None
-    parity = {"total_cost": int(per_graph.sum())}
+    parity = {"total_cost": int(per_graph.sum()) if per_graph is not None else None}
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from concurrent.futures import ThreadPoolExecutor
         from oracle import ko
-        k = min(num, 16)
-        sample = graphs[:k]
-        cores = min(16, os.cpu_count() or 1, k)
-        t1 = time.perf_counter()
-        with ThreadPoolExecutor(cores) as ex:
-            outs = list(ex.map(ko.reference_path, sample))
-        dt = time.perf_counter() - t1
+        cores = host_cores()
+        every = [gen.quincy(T, M, R, J, 1000 + k) for k in range(num)]
+
+        def all_graphs_cpu():
+            with ThreadPoolExecutor(cores) as ex:
+                return list(ex.map(ko.reference_path, every))
+        med, ts, outs, _ = timed_cpu(all_graphs_cpu, reps=args.cpu_reps, pin=False)
         m2 = gen.quincy_sizes(T, M, R, J)[1]
-        cpu = {"value": round(k * m2 / dt, 1), "unit": "arcs/s", "cores": cores, "kind": "port",
-               "sample": f"reference path (export -> SSP -> f lines -> BFS) on the first {k} of the {num} graphs, "
-                         f"one graph per thread on {cores} threads, {dt:.2f} s"}
-        parity.update({"checked_graphs": k, "match": bool(all(o[1] == int(c) for o, c in zip(outs, per_graph[:k])))})
-    mode = ("one device solve of their disjoint union" if args.batch_mode == "union"
-            else f"one context each, solved concurrently ({args.workers} workers/GPU)")
+        cpu = {"value": round(num * m2 / med, 1), "unit": "arcs/s", "cores": cores, "kind": "port",
+               "sample": f"all {num} graphs through the restatement of the reference CPU path (export -> SSP -> "
+                         f"f lines -> BFS), one graph per thread on {cores} threads (the host cores this process "
+                         f"may use), median of {len(ts)} after 1 warm-up",
+               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts)}
+        parity.update({"checked_graphs": num,
+                       "match": bool(per_graph is not None and all(o[1] == int(c) for o, c in zip(outs, per_graph)))})
+    mode = {"abi": "C-ABI batch (union per device, RCCL gather inside libksmcmf)",
+            "union": "one device solve of their disjoint union",
+            "streams": f"one context each, solved concurrently ({args.workers} workers/GPU)"}[args.batch_mode]
     config = {"workload": f"config5: {num} independent config-2 graphs (T={T} M={M}, seeds 1000..{999 + num}) "
                           f"round-robin over {D.world} GPU(s), {mode}; step = every graph solved once",
               "graphs": num, "tasks": T, "machines": M, "graphs_per_gpu": len(mine), "mode": args.batch_mode,
@@ -351,8 +423,11 @@ def run_batch(args, D):
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
                      roofline=roofline_of(results), cpu_baseline=cpu, gather=gather, parity=parity,
                      solve=dict(results[-1].raw))
-    for c in ctxs:
-        c.close()
+    if args.batch_mode == "abi":
+        bt.close()
+    else:
+        for c in ctxs:
+            c.close()
     return line
 
 
@@ -365,9 +440,10 @@ def main():
     ap.add_argument("--config", default="config3", choices=sorted(gen.CONFIGS))
     ap.add_argument("--graphs", type=int, default=64)
     ap.add_argument("--workers", type=int, default=4)
-    ap.add_argument("--batch-mode", default="union", choices=["union", "streams"])
+    ap.add_argument("--batch-mode", default="abi", choices=["abi", "union", "streams"])
     ap.add_argument("--warm", type=int, default=0, help="incremental workload: warm-start re-solves")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--cpu-reps", type=int, default=5, help="CPU baseline: median of this many after 1 warm-up")
     ap.add_argument("--alpha", type=int, default=0)
     ap.add_argument("--gu-interval", type=int, default=0)
     ap.add_argument("--price-refine", type=int, default=-1)

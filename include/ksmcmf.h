@@ -290,6 +290,36 @@ int ks_topology_stats(ks_ctx* ctx, uint64_t max_tasks_per_pu, const uint64_t* pu
                       const uint64_t* pu_running, size_t k, uint64_t* slots_below,
                       uint64_t* running_below, size_t cap, size_t* count);
 
+/* ---- config 5: independent graphs sharded over GPUs (SURVEY §7 step 6, §8 row e) --
+ * No reference counterpart (ksched solves one graph per round,
+ * flowscheduler/scheduler.go:350); this is the north star's multi-GPU mode: cluster
+ * cells / what-if graphs, graph g on global rank g mod world, each device solving
+ * the disjoint union of its graphs, then ONE collective — every rank's per-graph
+ * rows to rank 0 over RCCL (ncclSend/ncclRecv in a group), inside the library. */
+typedef struct ks_batch ks_batch;
+#define KS_UNIQUE_ID_BYTES 128
+
+/* One process driving several devices (ncclCommInitAll over devices[0..ndev)). */
+ks_batch*   ks_batch_create(const int* devices, int ndev, const ks_opts* opts);
+/* One process per GPU (e.g. under torch.distributed.run): rank 0 makes the id with
+ * ks_batch_unique_id and shares it out of band; every rank then calls this. */
+int         ks_batch_unique_id(uint8_t* id /* KS_UNIQUE_ID_BYTES */);
+ks_batch*   ks_batch_create_rank(int device, int nranks, int rank, const uint8_t* id, const ks_opts* opts);
+void        ks_batch_destroy(ks_batch* b);
+const char* ks_batch_last_error(ks_batch* b);
+/* Every rank passes ALL ngraphs graphs (arrays as for ks_load_graph); each device
+ * uploads the ones it owns. */
+int ks_batch_load(ks_batch* b, size_t ngraphs, const ks_node* const* nodes, const size_t* n,
+                  const ks_arc* const* arcs, const size_t* m);
+/* Solve every local device's union concurrently; results[i] (may be NULL) for the
+ * i-th local device. */
+int ks_batch_solve(ks_batch* b, ks_result* results);
+/* Collective (all ranks call it): per graph its cost, flow value and the PU node id
+ * (local to the graph, 0 = unscheduled) of each of its task nodes in id order,
+ * gathered to global rank 0, whose pu[g·max_tasks ..], cost[g], flow[g] receive
+ * them (other ranks may pass NULL). */
+int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, int64_t* flow);
+
 #ifdef __cplusplus
 }
 #endif

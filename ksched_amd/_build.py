@@ -10,9 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libksmcmf.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("ks_engine.hip", "ks_store.hip", "ks_sched.hip", "ks_host.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "ks_engine.h"), os.path.join(CSRC, "ks_store.h"), os.path.join(CSRC, "ks_sched.h"),
-                  os.path.join(ROOT, "include", "ksmcmf.h")]
+SOURCES = [os.path.join(CSRC, f) for f in ("ks_engine.hip", "ks_store.hip", "ks_sched.hip", "ks_batch.hip",
+                                           "ks_host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("ks_engine.h", "ks_store.h", "ks_sched.h", "ks_ctx.h")] + [
+    os.path.join(ROOT, "include", "ksmcmf.h")]
 
 
 def hipcc() -> str:
@@ -36,7 +37,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"),
-           *SOURCES, "-o", tmp]
+           *SOURCES, "-ldl", "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -69,7 +70,7 @@ def build_variant(tag: str, defines: list[str]) -> str:
     out = variant_path(tag)
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines],
-           *SOURCES, "-o", out + ".tmp"]
+           *SOURCES, "-ldl", "-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out

@@ -1,0 +1,365 @@
+// ks_batch.hip — config 5 behind the C-ABI: independent cell graphs sharded over
+// GPUs, solved concurrently, and their task→PU mappings gathered to rank 0 over
+// RCCL inside libksmcmf (SURVEY §7 step 6, §8 row e).
+//
+// A single solve does not shard, so multi-GPU throughput comes
+// from independent graphs (cluster cells, what-if variants). Graph g belongs to
+// global rank g mod world (round-robin); each device solves the
+// disjoint union of its graphs as ONE device solve (the min-cost flow of a
+// disjoint union is the union of the optima). After the solves every device
+// packs one row per graph — [cost, flow value, PU id of each task (cell-local,
+// 0 = unscheduled)] — and rank 0 receives every device's rows with
+// ncclSend/ncclRecv in one group: a single collective, no data-path exchange.
+// Two ways to build the communicator: ks_batch_create (one process, several
+// devices: ncclCommInitAll) and ks_batch_create_rank (one process per GPU, e.g.
+// under torch.distributed.run: ncclCommInitRank with an id from rank 0).
+// RCCL is loaded with dlopen on the first batch (the single-graph API never
+// needs it); a process that already holds RCCL (torch) shares its copy.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ks_ctx.h"
+
+namespace {
+
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+
+    bool load(std::string& err) {
+        if (h) return true;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (h) break;
+        }
+        if (!h) {
+            err = std::string("RCCL not found: ") + dlerror();
+            return false;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            ok = ok && fn;
+        };
+        sym(GetUniqueId, "ncclGetUniqueId");
+        sym(CommInitAll, "ncclCommInitAll");
+        sym(CommInitRank, "ncclCommInitRank");
+        sym(CommDestroy, "ncclCommDestroy");
+        sym(GroupStart, "ncclGroupStart");
+        sym(GroupEnd, "ncclGroupEnd");
+        sym(Send, "ncclSend");
+        sym(Recv, "ncclRecv");
+        sym(GetErrorString, "ncclGetErrorString");
+        if (!ok) err = "RCCL is missing a symbol";
+        return ok;
+    }
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    return r;
+}
+
+// row r: PU ids of its tasks made cell-local (subtract the cell's node offset)
+__global__ void k_localize(int rows, int rowlen, const long long* __restrict__ off, long long* __restrict__ buf) {
+    const int r = blockIdx.y;
+    if (r >= rows) return;
+    long long* row = buf + (size_t)r * rowlen;
+    for (int i = 2 + blockIdx.x * blockDim.x + threadIdx.x; i < rowlen; i += gridDim.x * blockDim.x)
+        if (row[i] > 0) row[i] -= off[r];
+}
+
+}  // namespace
+
+struct ks_batch {
+    struct Local {
+        int device = 0;
+        int grank = 0;                  // global rank
+        ks_ctx* ctx = nullptr;
+        ncclComm_t comm = nullptr;
+        std::vector<int> graphs;        // graph ids solved here, in order
+        std::vector<int64_t> off;       // node-id offset of each graph in the union (+ total)
+        std::vector<int64_t> toff;      // task offset of each graph in the dense task vector (+ total)
+        long long* rows = nullptr;      // device: graphs.size() × rowlen
+        long long* scratch = nullptr;   // device: dense task→PU vector, offsets
+        size_t rows_cap = 0, scratch_cap = 0;
+        ks_result res{};
+    };
+    std::vector<Local> loc;
+    int world = 1;
+    size_t ngraphs = 0;
+    std::string err;
+    long long* root_buf = nullptr;      // rank 0: world × slots × rowlen
+    size_t root_cap = 0;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+};
+
+namespace {
+
+#define KB_HIP(expr)                                                          \
+    do {                                                                      \
+        hipError_t _e = (expr);                                               \
+        if (_e != hipSuccess) return b->fail(KS_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define KB_NCCL(expr)                                                         \
+    do {                                                                      \
+        ncclResult_t _r = (expr);                                             \
+        if (_r != ncclSuccess) return b->fail(KS_E_DEVICE, std::string(#expr) + ": " + rccl().GetErrorString(_r)); \
+    } while (0)
+
+ks_batch* make_batch(int world, const ks_opts* opts, const std::vector<std::pair<int, int>>& dev_rank) {
+    ks_batch* b = new (std::nothrow) ks_batch;
+    if (!b) return nullptr;
+    b->world = world;
+    for (auto [dev, rank] : dev_rank) {
+        ks_batch::Local l;
+        l.device = dev;
+        l.grank = rank;
+        l.ctx = ks_create(dev, opts);
+        if (!l.ctx) {
+            for (auto& x : b->loc) ks_destroy(x.ctx);
+            delete b;
+            return nullptr;
+        }
+        b->loc.push_back(std::move(l));
+    }
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ks_batch_unique_id(uint8_t* id) {
+    std::string err;
+    if (!id || !rccl().load(err)) return KS_E_DEVICE;
+    ncclUniqueId u;
+    if (rccl().GetUniqueId(&u) != ncclSuccess) return KS_E_DEVICE;
+    std::memcpy(id, u.internal, KS_UNIQUE_ID_BYTES);
+    return KS_OK;
+}
+
+ks_batch* ks_batch_create(const int* devices, int ndev, const ks_opts* opts) {
+    std::string err;
+    if (!devices || ndev < 1 || !rccl().load(err)) return nullptr;
+    std::vector<std::pair<int, int>> dr;
+    for (int i = 0; i < ndev; ++i) dr.emplace_back(devices[i], i);
+    ks_batch* b = make_batch(ndev, opts, dr);
+    if (!b) return nullptr;
+    std::vector<ncclComm_t> comms(ndev);
+    if (rccl().CommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
+        ks_batch_destroy(b);
+        return nullptr;
+    }
+    for (int i = 0; i < ndev; ++i) b->loc[i].comm = comms[i];
+    return b;
+}
+
+ks_batch* ks_batch_create_rank(int device, int nranks, int rank, const uint8_t* id, const ks_opts* opts) {
+    std::string err;
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks || !rccl().load(err)) return nullptr;
+    ks_batch* b = make_batch(nranks, opts, {{device, rank}});
+    if (!b) return nullptr;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, KS_UNIQUE_ID_BYTES);
+    if (hipSetDevice(device) != hipSuccess || rccl().CommInitRank(&b->loc[0].comm, nranks, u, rank) != ncclSuccess) {
+        ks_batch_destroy(b);
+        return nullptr;
+    }
+    return b;
+}
+
+void ks_batch_destroy(ks_batch* b) {
+    if (!b) return;
+    for (auto& l : b->loc) {
+        (void)hipSetDevice(l.device);
+        if (l.comm) rccl().CommDestroy(l.comm);
+        if (l.rows) (void)hipFree(l.rows);
+        if (l.scratch) (void)hipFree(l.scratch);
+        ks_destroy(l.ctx);
+    }
+    if (b->root_buf) {
+        (void)hipSetDevice(b->loc[0].device);
+        (void)hipFree(b->root_buf);
+    }
+    delete b;
+}
+
+const char* ks_batch_last_error(ks_batch* b) { return b ? b->err.c_str() : "null batch"; }
+
+int ks_batch_load(ks_batch* b, size_t ngraphs, const ks_node* const* nodes, const size_t* n,
+                  const ks_arc* const* arcs, const size_t* m) {
+    if (!b) return KS_E_INVALID;
+    if (ngraphs && (!nodes || !n || !arcs || !m)) return b->fail(KS_E_INVALID, "null graph arrays");
+    b->ngraphs = ngraphs;
+    for (auto& l : b->loc) {
+        l.graphs.clear();
+        for (size_t g = (size_t)l.grank; g < ngraphs; g += (size_t)b->world) l.graphs.push_back((int)g);
+        if (l.graphs.size() > 1024) return b->fail(KS_E_INVALID, "more than 1024 graphs on one device");
+        // the disjoint union of this device's graphs: node ids offset per graph
+        std::vector<ks_node> un;
+        std::vector<ks_arc> ua;
+        l.off.assign(1, 0);
+        l.toff.assign(1, 0);
+        for (int g : l.graphs) {
+            uint64_t maxid = 0;
+            int64_t tasks = 0;
+            for (size_t i = 0; i < n[g]; ++i) {
+                ks_node x = nodes[g][i];
+                maxid = std::max<uint64_t>(maxid, x.id);
+                tasks += x.type == KS_NODE_TASK;
+                x.id += (uint64_t)l.off.back();
+                un.push_back(x);
+            }
+            for (size_t i = 0; i < m[g]; ++i) {
+                ks_arc a = arcs[g][i];
+                a.src += (uint64_t)l.off.back();
+                a.dst += (uint64_t)l.off.back();
+                ua.push_back(a);
+            }
+            l.off.push_back(l.off.back() + (int64_t)maxid);
+            l.toff.push_back(l.toff.back() + tasks);
+        }
+        const int rc = ks_load_graph(l.ctx, un.data(), un.size(), ua.data(), ua.size());
+        if (rc) return b->fail(rc, ks_last_error(l.ctx));
+    }
+    return KS_OK;
+}
+
+int ks_batch_solve(ks_batch* b, ks_result* results) {
+    if (!b) return KS_E_INVALID;
+    std::vector<int> rcs(b->loc.size(), KS_OK);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < b->loc.size(); ++i)
+        th.emplace_back([&, i]() { rcs[i] = ks_solve(b->loc[i].ctx, &b->loc[i].res); });
+    for (auto& t : th) t.join();
+    for (size_t i = 0; i < b->loc.size(); ++i) {
+        if (results) results[i] = b->loc[i].res;
+        if (rcs[i]) return b->fail(rcs[i], ks_last_error(b->loc[i].ctx));
+    }
+    return KS_OK;
+}
+
+int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, int64_t* flow) {
+    if (!b) return KS_E_INVALID;
+    const size_t rowlen = 2 + max_tasks;
+    const size_t slots = (b->ngraphs + b->world - 1) / std::max(1, b->world);
+    const size_t block = std::max<size_t>(1, slots) * rowlen;   // elements per rank
+    bool has_root = false;
+    // 1. every device packs its rows: [cost, flow value, cell-local PU per task]
+    for (auto& l : b->loc) {
+        KB_HIP(hipSetDevice(l.device));
+        if (l.grank == 0) has_root = true;
+        ks_ctx* c = l.ctx;
+        const size_t k = l.graphs.size();
+        for (size_t i = 0; i < k; ++i)
+            if ((size_t)(l.toff[i + 1] - l.toff[i]) > max_tasks)
+                return b->fail(KS_E_INVALID, "a graph has more tasks than max_tasks");
+        hipStream_t st = c->eng.stream();
+        if (l.rows_cap < block) {
+            if (l.rows) (void)hipFree(l.rows);
+            l.rows = nullptr;
+            KB_HIP(hipMalloc(&l.rows, block * sizeof(long long)));
+            l.rows_cap = block;
+        }
+        const size_t need = (size_t)l.toff.back() + 3 * (k + 1);
+        if (l.scratch_cap < need) {
+            if (l.scratch) (void)hipFree(l.scratch);
+            l.scratch = nullptr;
+            KB_HIP(hipMalloc(&l.scratch, std::max<size_t>(need, 1) * sizeof(long long)));
+            l.scratch_cap = need;
+        }
+        KB_HIP(hipMemsetAsync(l.rows, 0, block * sizeof(long long), st));
+        if (!k) continue;
+        long long* dcost = l.scratch + l.toff.back();
+        long long* dflow = dcost + (k + 1);
+        long long* doff = dflow + (k + 1);
+        int rc = c->eng.cell_sums(l.off.data(), k, (int64_t*)dcost, (int64_t*)dflow, c->err);
+        size_t cnt = 0;
+        if (rc == KS_OK) rc = ks_get_task_pu_device(c, (uint64_t*)l.scratch, (size_t)l.toff.back(), &cnt);
+        if (rc) return b->fail(rc, ks_last_error(c));
+        KB_HIP(hipMemcpy2DAsync(l.rows, rowlen * sizeof(long long), dcost, sizeof(long long), sizeof(long long), k,
+                                hipMemcpyDeviceToDevice, st));
+        KB_HIP(hipMemcpy2DAsync(l.rows + 1, rowlen * sizeof(long long), dflow, sizeof(long long), sizeof(long long), k,
+                                hipMemcpyDeviceToDevice, st));
+        for (size_t i = 0; i < k; ++i) {
+            const size_t t = (size_t)(l.toff[i + 1] - l.toff[i]);
+            if (t)
+                KB_HIP(hipMemcpyAsync(l.rows + i * rowlen + 2, l.scratch + l.toff[i], t * sizeof(long long),
+                                      hipMemcpyDeviceToDevice, st));
+        }
+        KB_HIP(hipMemcpyAsync(doff, l.off.data(), k * sizeof(long long), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_localize, dim3(std::max<size_t>(1, std::min<size_t>(64, (rowlen + 255) / 256)), k),
+                           dim3(256), 0, st, (int)k, (int)rowlen, (const long long*)doff, l.rows);
+        KB_HIP(hipGetLastError());
+        KB_HIP(hipStreamSynchronize(st));
+    }
+    // 2. one group: every rank's rows to global rank 0
+    long long* rbuf = nullptr;
+    for (auto& l : b->loc)
+        if (l.grank == 0) {
+            KB_HIP(hipSetDevice(l.device));
+            const size_t need = block * (size_t)b->world;
+            if (b->root_cap < need) {
+                if (b->root_buf) (void)hipFree(b->root_buf);
+                b->root_buf = nullptr;
+                KB_HIP(hipMalloc(&b->root_buf, need * sizeof(long long)));
+                b->root_cap = need;
+            }
+            rbuf = b->root_buf;
+            KB_HIP(hipMemcpyAsync(rbuf, l.rows, block * sizeof(long long), hipMemcpyDeviceToDevice, l.ctx->eng.stream()));
+        }
+    if (b->world > 1) {
+        KB_NCCL(rccl().GroupStart());
+        for (auto& l : b->loc) {
+            hipStream_t st = l.ctx->eng.stream();
+            if (l.grank == 0) {
+                for (int r = 1; r < b->world; ++r)
+                    KB_NCCL(rccl().Recv(rbuf + (size_t)r * block, block, ncclInt64, r, l.comm, st));
+            } else {
+                KB_NCCL(rccl().Send(l.rows, block, ncclInt64, 0, l.comm, st));
+            }
+        }
+        KB_NCCL(rccl().GroupEnd());
+    }
+    for (auto& l : b->loc) {
+        KB_HIP(hipSetDevice(l.device));
+        KB_HIP(hipStreamSynchronize(l.ctx->eng.stream()));
+    }
+    if (!has_root) return KS_OK;
+    // 3. rank 0: rows back in graph order
+    std::vector<long long> host(block * (size_t)b->world);
+    for (auto& l : b->loc)
+        if (l.grank == 0) {
+            KB_HIP(hipSetDevice(l.device));
+            KB_HIP(hipMemcpy(host.data(), rbuf, host.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        }
+    for (size_t g = 0; g < b->ngraphs; ++g) {
+        const long long* row = host.data() + (g % b->world) * block + (g / b->world) * rowlen;
+        if (cost) cost[g] = row[0];
+        if (flow) flow[g] = row[1];
+        if (pu) std::memcpy(pu + g * max_tasks, row + 2, max_tasks * sizeof(uint64_t));
+    }
+    return KS_OK;
+}
+
+}  // extern "C"

@@ -45,6 +45,13 @@ public:
     // place (the previous solve's, edited by the deltas since).
     int solve(ks_result& r, bool warm, std::string& err);
 
+    // Per-partition sums of the last solve for a disjoint union of graphs: graph i
+    // owns node ids (off[i], off[i+1]]; cost[i] = Σ flow·cost over its arcs, flow[i] =
+    // net inflow into its demand nodes. off has k+1 entries (host); outputs are
+    // device pointers (k int64 each).
+    int cell_sums(const int64_t* off, size_t k, int64_t* dev_cost, int64_t* dev_flow, std::string& err);
+    hipStream_t stream() const;
+
     // Live arcs of the store (1-based ids), arc-slot order.
     int arcs(std::vector<ks_arc>& out, std::string& err);
 

@@ -1662,6 +1662,40 @@ __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, con
     }
 }
 
+// Per-partition cost and flow value of a disjoint union (k ≤ 1024 parts; one LDS
+// accumulator per part and block, one atomic per part and block).
+constexpr int MAX_CELLS = 1024;
+__global__ void k_cell_sums(int hi, int k, const long long* __restrict__ off, const unsigned char* __restrict__ alive,
+                            const int* __restrict__ src, const int* __restrict__ dst,
+                            const long long* __restrict__ supply, const long long* __restrict__ cost,
+                            const long long* __restrict__ flows, long long* __restrict__ out_cost,
+                            long long* __restrict__ out_flow) {
+    __shared__ long long sc[MAX_CELLS], sf[MAX_CELLS];
+    for (int i = threadIdx.x; i < k; i += BLK) sc[i] = sf[i] = 0;
+    __syncthreads();
+    for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
+        if (!alive[s]) continue;
+        const long long f = flows[s];
+        if (!f) continue;
+        const long long id = (long long)src[s] + 1;
+        int lo = 0, hh = k;   // the part j with off[j] < id <= off[j+1]
+        while (hh - lo > 1) {
+            const int mid = (lo + hh) >> 1;
+            if (off[mid] < id) lo = mid; else hh = mid;
+        }
+        __hip_atomic_fetch_add(&sc[lo], f * cost[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        long long fv = 0;
+        if (supply[dst[s]] < 0) fv += f;
+        if (supply[src[s]] < 0) fv -= f;
+        if (fv) __hip_atomic_fetch_add(&sf[lo], fv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < k; i += BLK) {
+        if (sc[i]) atom_add(&out_cost[i], sc[i]);
+        if (sf[i]) atom_add(&out_flow[i], sf[i]);
+    }
+}
+
 struct SlotAlive {
     const unsigned char* alive;
     __host__ __device__ bool operator()(const int& s) const { return alive[s] != 0; }
@@ -2717,6 +2751,35 @@ int Engine::arcs(std::vector<ks_arc>& out, std::string& err) {
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(d);
     KS_CHECK(e);
+    return KS_OK;
+}
+
+hipStream_t Engine::stream() const { return p_->stream; }
+
+int Engine::cell_sums(const int64_t* off, size_t k, int64_t* dev_cost, int64_t* dev_flow, std::string& err) {
+    EngineImpl& s = *p_;
+    if (!s.solved) {
+        err = "no successful solve";
+        return KS_E_INVALID;
+    }
+    if (k > (size_t)MAX_CELLS) {
+        err = "more than 1024 graphs in one union";
+        return KS_E_INVALID;
+    }
+    KS_CHECK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    const int hi = s.hi();
+    KS_CHECK(s.sched_u.ensure(k + 1));
+    KS_CHECK(hipMemcpyAsync(s.sched_u.p, off, (k + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    KS_CHECK(hipMemsetAsync(dev_cost, 0, k * sizeof(int64_t), st));
+    KS_CHECK(hipMemsetAsync(dev_flow, 0, k * sizeof(int64_t), st));
+    if (hi && k)
+        hipLaunchKernelGGL(k_cell_sums, dim3(grid_for(hi, 1024)), dim3(BLK), 0, st, hi, (int)k,
+                           (const long long*)s.sched_u.p, (const unsigned char*)s.a_alive.p, (const int*)s.a_src.p,
+                           (const int*)s.a_dst.p, (const long long*)s.n_supply.p, (const long long*)s.a_cost.p,
+                           (const long long*)s.flows.p, (long long*)dev_cost, (long long*)dev_flow);
+    KS_CHECK(hipGetLastError());
+    KS_CHECK(hipStreamSynchronize(st));
     return KS_OK;
 }
 

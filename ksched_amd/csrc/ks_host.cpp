@@ -23,16 +23,11 @@
 #include <vector>
 
 #include "../../include/ksmcmf.h"
-#include "ks_engine.h"
+#include "ks_ctx.h"
 
 namespace {
 
-struct NodeRec {
-    int64_t excess = 0;
-    int32_t type = 0;
-    bool alive = false;
-    bool pad = false;
-};
+
 
 
 constexpr uint64_t kMaxId = (1ULL << 30);
@@ -117,31 +112,6 @@ private:
 };
 
 }  // namespace
-
-struct ks_ctx {
-    ks::Engine eng;
-    ks_opts opts{};
-    std::string err;
-
-    std::vector<NodeRec> nodes;            // index = NodeID (slot 0 unused)
-    std::vector<uint32_t> epoch_of;        // per id: last apply that touched it
-    std::vector<int32_t> lastrm_of;        // per id: last REMOVE position in that apply
-    uint32_t epoch = 0;
-    int64_t sum_others = 0;                // Σ supply of live non-sink nodes
-    int64_t n_sinks = 0;
-    uint64_t sink_id = 0;                  // the sink (when n_sinks == 1)
-    int64_t n_tasks = 0;                   // live task nodes
-    int64_t dev_sink_supply = 0;           // the sink's supply as the device has it
-    bool have_solution = false;
-    bool flows_fresh = false;
-    std::vector<ks_flow> flows;
-
-    int fail(int code, const std::string& msg) {
-        err = msg;
-        return code;
-    }
-    int64_t nslots() const { return (int64_t)nodes.size() - 1; }
-};
 
 namespace {
 

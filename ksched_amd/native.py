@@ -21,6 +21,8 @@ EXPORTED_SYMBOLS = (
     "ks_apply_deltas", "ks_solve", "ks_get_flows", "ks_get_task_mapping", "ks_get_task_pu_device", "ks_solve_many",
     "ks_coalesce_deltas", "ks_get_store_stats", "ks_set_bindings", "ks_scheduling_deltas",
     "ks_update_unsched_costs", "ks_topology_stats", "ks_get_graph",
+    "ks_batch_create", "ks_batch_create_rank", "ks_batch_unique_id", "ks_batch_destroy", "ks_batch_last_error",
+    "ks_batch_load", "ks_batch_solve", "ks_batch_gather",
 )
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
@@ -124,6 +126,17 @@ def load(build_if_missing: bool = True):
     L.ks_coalesce_deltas.argtypes = [V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]
     L.ks_get_store_stats.argtypes = [V, P(KsStoreStats)]
     L.ks_get_graph.argtypes = [V, V, C.c_size_t, P(C.c_size_t), V, C.c_size_t, P(C.c_size_t)]
+    L.ks_batch_create.argtypes = [P(C.c_int), C.c_int, P(KsOpts)]
+    L.ks_batch_create.restype = V
+    L.ks_batch_create_rank.argtypes = [C.c_int, C.c_int, C.c_int, V, P(KsOpts)]
+    L.ks_batch_create_rank.restype = V
+    L.ks_batch_unique_id.argtypes = [V]
+    L.ks_batch_destroy.argtypes = [V]
+    L.ks_batch_last_error.argtypes = [V]
+    L.ks_batch_last_error.restype = C.c_char_p
+    L.ks_batch_load.argtypes = [V, C.c_size_t, P(V), P(C.c_size_t), P(V), P(C.c_size_t)]
+    L.ks_batch_solve.argtypes = [V, P(KsResult)]
+    L.ks_batch_gather.argtypes = [V, C.c_size_t, V, V, V]
     L.ks_set_bindings.argtypes = [V, V, V, C.c_size_t]
     L.ks_scheduling_deltas.argtypes = [V, C.c_int, V, C.c_size_t, P(C.c_size_t)]
     L.ks_update_unsched_costs.argtypes = [V, V, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_size_t)]
@@ -284,6 +297,95 @@ class Context:
         cnt = C.c_size_t()
         self._check(self._L.ks_get_task_pu_device(self._h, C.c_void_p(dev_ptr), cap, C.byref(cnt)))
         return cnt.value
+
+
+def graph_arrays(g):
+    """gen.Graph → (NODE_DT, ARC_DT) arrays with 1-based ids."""
+    nodes = np.zeros(g.n, NODE_DT)
+    nodes["id"] = np.arange(1, g.n + 1, dtype=np.uint64)
+    nodes["excess"] = g.supply
+    nodes["type"] = g.ntype
+    arcs = np.zeros(g.m, ARC_DT)
+    arcs["src"], arcs["dst"] = g.src, g.dst
+    arcs["low"], arcs["cap"], arcs["cost"] = g.low, g.cap, g.cost
+    arcs["type"] = g.arc_types()
+    return nodes, arcs
+
+
+class Batch:
+    """Config 5 through the C-ABI (ks_batch_*): independent graphs, graph g on
+    global rank g mod world, each device solving the union of its graphs; the
+    per-graph rows gathered to rank 0 over RCCL inside libksmcmf.
+
+    Batch(devices=[0, 1, ...]) drives several devices from one process;
+    Batch(device=d, world=W, rank=r, uid=bytes) is one rank of a
+    process-per-GPU job (uid from Batch.unique_id() on rank 0)."""
+
+    def __init__(self, devices=None, device: int = 0, world: int = 1, rank: int = 0, uid: bytes | None = None,
+                 **opts):
+        self._L = load()
+        self.opts = default_opts(**opts)
+        if uid is None:
+            devs = list(devices if devices is not None else [device])
+            arr = (C.c_int * len(devs))(*devs)
+            h = self._L.ks_batch_create(arr, len(devs), C.byref(self.opts))
+            self.local = len(devs)
+        else:
+            buf = C.create_string_buffer(bytes(uid), 128)
+            h = self._L.ks_batch_create_rank(device, world, rank, buf, C.byref(self.opts))
+            self.local = 1
+        if not h:
+            raise KsError(KS_E_DEVICE, "ks_batch_create failed (device or RCCL unavailable)")
+        self._h = h
+        self.ngraphs = 0
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        rc = load().ks_batch_unique_id(buf)
+        if rc != KS_OK:
+            raise KsError(rc, "ks_batch_unique_id failed")
+        return buf.raw
+
+    def _check(self, rc):
+        if rc != KS_OK:
+            raise KsError(rc, self._L.ks_batch_last_error(self._h).decode(errors="replace"))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ks_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, graphs):
+        arrs = [graph_arrays(g) for g in graphs]
+        k = len(arrs)
+        self._keep = arrs
+        npt = (C.c_void_p * max(1, k))(*[a[0].ctypes.data for a in arrs])
+        apt = (C.c_void_p * max(1, k))(*[a[1].ctypes.data for a in arrs])
+        ns = (C.c_size_t * max(1, k))(*[a[0].shape[0] for a in arrs])
+        ms = (C.c_size_t * max(1, k))(*[a[1].shape[0] for a in arrs])
+        self._check(self._L.ks_batch_load(self._h, k, npt, ns, apt, ms))
+        self.ngraphs = k
+
+    def solve(self) -> list[SolveResult]:
+        rs = (KsResult * self.local)()
+        self._check(self._L.ks_batch_solve(self._h, rs))
+        return [SolveResult(r.total_cost, r.flow_value, r.as_dict()) for r in rs]
+
+    def gather(self, max_tasks: int, root: bool = True):
+        """→ (pu [ngraphs, max_tasks] uint64, cost [ngraphs], flow [ngraphs]) on rank 0."""
+        pu = np.zeros((self.ngraphs, max_tasks), np.uint64) if root else None
+        cost = np.zeros(self.ngraphs, np.int64) if root else None
+        flow = np.zeros(self.ngraphs, np.int64) if root else None
+        p = lambda a: None if a is None else a.ctypes.data
+        self._check(self._L.ks_batch_gather(self._h, max_tasks, p(pu), p(cost), p(flow)))
+        return pu, cost, flow
 
 
 def solve_many(ctxs: list[Context], workers: int = 0) -> list[SolveResult]:

@@ -218,3 +218,27 @@ def test_deltas_applied_in_place_on_device():
             mp = ctx.task_mapping()
         assert rebuilt[0] == 1                 # the first stream switches the CSR to slack
         assert sum(rebuilt[1:]) <= 3, rebuilt  # then the slack absorbs most rounds
+
+
+def test_batch_c_abi_rccl_gather():
+    """Config 5 through the C-ABI (ks_batch_*: the disjoint union per device,
+    per-graph rows gathered to rank 0 over RCCL inside libksmcmf) on the box's
+    one device: per-graph cost and flow vs the oracle, cell-local PU ids valid."""
+    T, M, R, J = 3_000, 300, 12, 30
+    graphs = [gen.quincy(T, M, R, J, 1200 + i) for i in range(6)]
+    b = native.Batch(devices=[0])
+    try:
+        b.load(graphs)
+        res = b.solve()
+        assert len(res) == 1 and res[0].flow == 6 * T
+        pu, cost, flow = b.gather(T)
+        for i, g in enumerate(graphs):
+            st, c, f, _ = ko.cost_scaling(g)
+            assert st == 0 and (int(cost[i]), int(flow[i])) == (c, f)
+            tasks = np.nonzero(g.ntype == 1)[0] + 1
+            mp = {int(t): int(p) for t, p in zip(tasks, pu[i]) if p}
+            check_mapping(g, mp)
+            assert len(mp) > 0
+        assert int(res[0].cost) == int(cost.sum())
+    finally:
+        b.close()
