@@ -432,6 +432,11 @@ def run_batch(args, D):
 
 
 def main():
+    # stdout carries exactly one JSON line (rank 0): anything else a library prints
+    # there (RCCL's version banner at communicator init) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -453,7 +458,7 @@ def main():
     run = {"full": run_full, "incremental": run_incremental, "batch": run_batch}[args.workload]
     line = run(args, D)
     if D.rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     D.close()
 
 

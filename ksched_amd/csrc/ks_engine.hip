@@ -154,6 +154,7 @@ struct DG {
     Front bf[3];   // Bellman-Ford frontiers
     Ctl* ctl;
     unsigned long long* ctr;
+    unsigned long long* stamps;   // diagnostic builds (-DKS_STAMPS): per launch [first start, last end|kind]
 };
 
 // ---------------------------------------------------------------- atomics ---
@@ -1030,11 +1031,33 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
     }
 }
 
+#ifdef KS_STAMPS
+constexpr int STAMP_W = 10;
+// Diagnostic: per launch, the earliest block start and the latest end of a block
+// that did work, tagged with that block's kind (1 hub chunk, 2 chunked node,
+// 3 + c window class c).
+__device__ __forceinline__ void stamp(const DG& g, int id, unsigned long long t0, int busy, int kind) {
+    const int any = __syncthreads_or(busy);
+    if (threadIdx.x == 0 && any && g.stamps && id >= 0 && id < 8192) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* r = g.stamps + (size_t)STAMP_W * id;
+        atomicMin(&r[0], t0);
+        atomicMax(&r[1], (t1 << 4) | (unsigned long long)kind);
+        atomicMax(&r[2], t0);                       // latest start of a working block
+        atomicMax(&r[2 + kind], t1 - t0);           // longest block of this kind
+    }
+}
+#endif
+
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
     if (!g.ctl->bf_done) return;   // the preceding global update has not been applied
     if (!(pos == 0 ? g.ctl->apply_act : g.ctl->sweep_act[pos - 1])) return;   // empty frontier
+#ifdef KS_STAMPS
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+    int kind = 0;
+#endif
     const Front F = g.sf[seq % 3], N = g.sf[(seq + 1) % 3];
     const long long eps = g.ctl->eps;
     const long long* P = (pos & 1) ? g.p1 : g.p0;
@@ -1044,7 +1067,12 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     int out = 0;
     if ((int)blockIdx.x < g.nhitems) {
         const HItem it = g.hitems[blockIdx.x];
-        if (F.hub[it.hid]) hub_chunk(g, F, N, it, P, PN, eps, pd, out, c);
+        if (F.hub[it.hid]) {
+            hub_chunk(g, F, N, it, P, PN, eps, pd, out, c);
+#ifdef KS_STAMPS
+            kind = 1;
+#endif
+        }
     } else {
         const int tw = ((int)gridDim.x - g.nhitems) * WPB;
         const int w0 = wave_index_in_grid(g.nhitems);
@@ -1058,8 +1086,14 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             if (w >= g.wbeg[CCLS]) {
                 const CItem ci = g.citems[w - g.wbeg[CCLS]];
                 if (ci.lead) node_discharge<8>(g, F, N, ci.node, P, PN, eps, pd, out, c);
+#ifdef KS_STAMPS
+                kind = max(kind, 2);
+#endif
                 continue;
             }
+#ifdef KS_STAMPS
+            kind = max(kind, 3 + class_of_window(g, w));
+#endif
             switch (class_of_window(g, w)) {
                 case 0: sweep_win<0>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
                 case 1: sweep_win<1>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
@@ -1071,6 +1105,16 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     }
     if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
     flush_counters(g, c);
+#ifdef KS_STAMPS
+    {   // the block's kind = the max over its waves
+        __shared__ int sk[WPB];
+        if (lane_id() == 0) sk[threadIdx.x >> 6] = kind;
+        __syncthreads();
+        int k2 = 0;
+        for (int i = 0; i < WPB; ++i) k2 = max(k2, sk[i]);
+        stamp(g, seq & 4095, ts0, kind > 0, k2);
+    }
+#endif
 }
 
 // ================================================ Bellman-Ford (GU and PR) ===
@@ -1261,6 +1305,9 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     const Front F = g.bf[seq % 3], N = g.bf[(seq + 1) % 3];
     if (threadIdx.x < HUB_LDS) hub_min[threadIdx.x] = INF64;
     __syncthreads();
+#ifdef KS_STAMPS
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const long long eps = g.ctl->eps;
     int out = 0;
     long long scans = 0;
@@ -1339,6 +1386,9 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
         g.ctl->bf_count += 1;
     }
     scans = wave_sum(scans);
+#ifdef KS_STAMPS
+    stamp(g, 4096 + (seq & 4095), ts0, scans > 0, (int)blockIdx.x < g.nhitems ? 1 : 3);
+#endif
     if (lane_id() == 0 && scans) {
         const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
         atomicAdd(g.ctr + sh * NCTR + C_GUSCAN, (unsigned long long)scans);
@@ -1832,6 +1882,7 @@ struct EngineImpl {
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
+    DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;        // pinned host mirror
     long long* h_scr = nullptr;  // pinned scratch: [0] eps, [1] max |cost|
@@ -1995,6 +2046,7 @@ struct EngineImpl {
         }
         g.ctl = ctl.p;
         g.ctr = ctr.p;
+        g.stamps = stamps.n > 1 ? stamps.p : nullptr;
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
@@ -2872,6 +2924,16 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     KS_CHECK(hipEventRecord(s.ev[1], st));
 
     // ------------------------------------------------------------ phases ---
+#ifdef KS_STAMPS
+    const char* stamp_path = std::getenv("KS_STAMPS_OUT");
+    if (stamp_path) {
+        KS_CHECK(s.stamps.ensure(STAMP_W * 8192));
+        std::vector<unsigned long long> init(STAMP_W * 8192, 0);
+        for (int i = 0; i < 8192; ++i) init[STAMP_W * i] = ~0ULL;
+        KS_CHECK(hipMemcpyAsync(s.stamps.p, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
+        KS_CHECK(hipStreamSynchronize(st));
+    }
+#endif
     DG g = s.dg();
     {
         const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
@@ -3083,6 +3145,22 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
 
+#ifdef KS_STAMPS
+    if (stamp_path && s.stamps.n > 1) {
+        std::vector<unsigned long long> hs(STAMP_W * 8192);
+        KS_CHECK(hipMemcpy(hs.data(), s.stamps.p, hs.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(stamp_path, "a")) {
+            for (int i = 0; i < 8192; ++i) {
+                const unsigned long long* r = &hs[STAMP_W * i];
+                if (!r[1]) continue;
+                std::fprintf(f, "%d %llu %llu %llu %llu", i, r[0], r[1] >> 4, r[1] & 15, r[2] - r[0]);
+                for (int k = 3; k < STAMP_W; ++k) std::fprintf(f, " %llu", r[k]);
+                std::fprintf(f, "\n");
+            }
+            std::fclose(f);
+        }
+    }
+#endif
     res.total_cost = tot_cost;
     res.flow_value = tot_flow;
     res.phases = phases;

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace CSV (per-dispatch start/end): per kernel
+the duration distribution, and the idle gaps between consecutive dispatches.
+
+    python tools/kernel_trace.py <dir with *kernel_trace.csv> [--kernels k_sweep,k_bf_round]
+"""
+import csv
+import glob
+import os
+import re
+import sys
+
+import numpy as np
+
+
+def main():
+    d = sys.argv[1]
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r["Kernel_Name"]
+                m = re.search(r"(k_\w+(<\w+>)?)\(", name)
+                short = m.group(1) if m else name.replace("(anonymous namespace)", "")[:40]
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short))
+    rows.sort()
+    st = np.array([r[0] for r in rows], np.int64)
+    en = np.array([r[1] for r in rows], np.int64)
+    names = np.array([r[2] for r in rows])
+    dur = (en - st) / 1e3
+    gaps = np.maximum(0, st[1:] - en[:-1]) / 1e3
+    print(f"dispatches {len(rows)}, busy {dur.sum() / 1e3:.2f} ms, span {(en.max() - st.min()) / 1e6:.2f} ms")
+    for k in sorted(set(names), key=lambda k: -dur[names == k].sum()):
+        x = dur[names == k]
+        if x.sum() < 100:
+            continue
+        q = np.percentile(x, [10, 50, 90, 99])
+        print(f"{k[:40]:40s} n={len(x):6d} sum={x.sum() / 1e3:8.2f}ms p10={q[0]:6.1f} p50={q[1]:6.1f} "
+              f"p90={q[2]:6.1f} p99={q[3]:6.1f} us; <2us: {(x < 2).sum()}")
+    print(f"gaps: n={len(gaps)} sum={gaps.sum() / 1e3:.2f} ms p50={np.median(gaps):.2f} p90={np.percentile(gaps, 90):.2f} us")
+
+
+if __name__ == "__main__":
+    main()
