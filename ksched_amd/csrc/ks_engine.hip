@@ -622,8 +622,15 @@ __global__ void k_max_cost(int hi, const unsigned char* __restrict__ alive, cons
     long long mx = 0;
     for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK)
         if (alive[s]) mx = max(mx, cost[s] < 0 ? -cost[s] : cost[s]);
+    // one atomic per workgroup (per-wave atomics on one address serialise)
+    __shared__ long long sh[WPB];
     mx = wave_max(mx);
-    if (lane_id() == 0 && mx) __hip_atomic_fetch_max(out, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane_id() == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < WPB; ++i) mx = max(mx, sh[i]);
+        if (mx) __hip_atomic_fetch_max(out, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 struct ClassIs {
@@ -1032,12 +1039,15 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
 }
 
 #ifdef KS_STAMPS
-constexpr int STAMP_W = 10;
+constexpr int STAMP_W = 11;
 // Diagnostic: per launch, the earliest block start and the latest end of a block
 // that did work, tagged with that block's kind (1 hub chunk, 2 chunked node,
 // 3 + c window class c).
-__device__ __forceinline__ void stamp(const DG& g, int id, unsigned long long t0, int busy, int kind) {
+__device__ __forceinline__ void stamp(const DG& g, int id, unsigned long long t0, int busy, int kind,
+                                      unsigned long long work) {
     const int any = __syncthreads_or(busy);
+    work = wave_sum((long long)work);
+    if (lane_id() == 0 && work && g.stamps && id >= 0 && id < 8192) atomicAdd(&g.stamps[STAMP_W * id + 10], work);
     if (threadIdx.x == 0 && any && g.stamps && id >= 0 && id < 8192) {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         unsigned long long* r = g.stamps + (size_t)STAMP_W * id;
@@ -1112,7 +1122,7 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         __syncthreads();
         int k2 = 0;
         for (int i = 0; i < WPB; ++i) k2 = max(k2, sk[i]);
-        stamp(g, seq & 4095, ts0, kind > 0, k2);
+        stamp(g, seq & 4095, ts0, kind > 0, k2, (unsigned long long)c.visit);
     }
 #endif
 }
@@ -1307,6 +1317,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     __syncthreads();
 #ifdef KS_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+    int kind = (int)blockIdx.x < g.nhitems ? 1 : 0;
 #endif
     const long long eps = g.ctl->eps;
     int out = 0;
@@ -1358,8 +1369,14 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
                 bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
+#ifdef KS_STAMPS
+                kind = max(kind, 2);
+#endif
                 continue;
             }
+#ifdef KS_STAMPS
+            kind = max(kind, 3 + class_of_window(g, w));
+#endif
             switch (class_of_window(g, w)) {
                 case 0: bf_win<0, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
                 case 1: bf_win<1, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
@@ -1387,7 +1404,13 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     }
     scans = wave_sum(scans);
 #ifdef KS_STAMPS
-    stamp(g, 4096 + (seq & 4095), ts0, scans > 0, (int)blockIdx.x < g.nhitems ? 1 : 3);
+    {
+        __shared__ int sk[WPB];
+        if (lane_id() == 0) sk[threadIdx.x >> 6] = kind;
+        __syncthreads();
+        for (int i = 0; i < WPB; ++i) kind = max(kind, sk[i]);
+    }
+    stamp(g, 4096 + (seq & 4095), ts0, scans > 0, kind, (unsigned long long)(lane_id() == 0 ? scans : 0));
 #endif
     if (lane_id() == 0 && scans) {
         const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
@@ -2910,7 +2933,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     }
     // max |cost| → the first phase's ε
     if (hi)
-        hipLaunchKernelGGL(k_max_cost, dim3(grid_for(hi, 2048)), dim3(BLK), 0, st, hi,
+        hipLaunchKernelGGL(k_max_cost, dim3(grid_for(hi, 512)), dim3(BLK), 0, st, hi,
                            (const unsigned char*)s.a_alive.p, (const long long*)s.a_cost.p, &s.ctl.p->gu_L);
     KS_CHECK(hipMemcpyAsync(s.h_ctl, s.ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, st));
     KS_CHECK(hipStreamSynchronize(st));
@@ -2950,6 +2973,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
+    const bool cycle_log = std::getenv("KS_CYCLE_LOG") != nullptr;   // diagnostic: one stderr line per cycle
     long long eps = std::max<long long>(1, maxc * mult);
     uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0;
     double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
@@ -3067,6 +3091,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 continue;
             }
             gu_running = false;
+            if (cycle_log)
+                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d\n", phases, eps,
+                             s.h_ctl->bf_count - gu_r0, ev_ms(s.kev[0], s.kev[1]), ev_ms(s.kev[2], s.kev[3]),
+                             s.h_ctl->sweep_act[gi - 1]);
             kb = std::max(8, std::min(256, s.h_ctl->bf_count - gu_r0 + 6));
             ++gus;
             sweeps += gi;

@@ -67,6 +67,17 @@ def main():
             if len(d):
                 print(f"   longest {KINDS[k]:10s} block: in {len(d):5d} launches, p50 {np.median(d):6.1f} us "
                       f"p90 {np.percentile(d, 90):6.1f} us")
+    for name, sel, unit in (("sweep", rows[:, 0] < 4096, "active nodes"), ("bf", rows[:, 0] >= 4096, "arc scans")):
+        x = rows[sel]
+        span = (x[:, 2] - x[:, 1]) * 0.01
+        work = x[:, 12]
+        print(f"{name}: time by {unit} per launch")
+        edges = [0, 16, 64, 256, 1024, 4096, 16384, 65536, 1 << 40]
+        for lo, hi in zip(edges[:-1], edges[1:]):
+            m = (work >= lo) & (work < hi)
+            if m.any():
+                print(f"   [{lo:6d}, {hi if hi < 1 << 40 else 'inf'}): launches {m.sum():5d} "
+                      f"span p50 {np.median(span[m]):6.1f} us, sum {span[m].sum() / 1e3 / a.solves:6.2f} ms/solve")
     ctx.close()
 
 
