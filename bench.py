@@ -37,39 +37,56 @@ from ksched_amd import batch, churn, gen, native  # noqa: E402
 
 METRIC = "MCMF solve latency (ms) + arcs/s at 100k tasks x 10k machines, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
-B_UNIT = 24             # bytes per residual-arc scan / node visit / push
-B_RELAX = 44            # Bellman-Ford in-arc relaxation: ucap, rcap, cost (8 each), head (4),
-                        # gathered price and distance of the tail (8 each)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+B_UNIT = 24             # bytes per residual-arc scan / node visit / push / relaxation
+B_RELAX = 44            # Bellman-Ford in-arc relaxation as the kernel reads it: ucap, rcap, cost (8 each),
+                        # head (4), gathered price and distance of the tail (8 each) — second field
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def roofline_of(results):
     """HBM roofline of the dominant kernel (by event-timed device time) over the
-    timed steps: algorithmic bytes from the device counters divided
-    by the HIP-event-timed duration of that kernel's launches."""
+    timed steps: algorithmic bytes = SURVEY §8(d)'s 24 B per unit × the device
+    counters' units, divided by the HIP-event-timed duration of that kernel's
+    launches (measured on the engine's stream). For k_bf_round the 44 B the
+    relaxation actually reads is reported beside it. ``traffic`` (PMC bytes per
+    launch) cannot be collected inside this run (rocprofv3 --pmc is its own
+    pass): it is read from the dated profile named in ``traffic_source``."""
+    n_res = max(1, len(results))
     sw_ms = sum(r.raw["ms_sweep_kernels"] for r in results)
     bf_ms = sum(r.raw["ms_gu_kernels"] for r in results)
     sw_n = sum(r.raw["sweep_launches"] for r in results)
     bf_n = sum(r.raw["gu_launches"] for r in results)
-    sw_b = B_UNIT * sum(r.raw["arc_scans"] + r.raw["node_visits"] + r.raw["pushes"] for r in results)
-    bf_b = B_RELAX * sum(r.raw["gu_arc_scans"] for r in results)
+    sw_units = sum(r.raw["arc_scans"] + r.raw["node_visits"] + r.raw["pushes"] for r in results)
+    bf_units = sum(r.raw["gu_arc_scans"] for r in results)
     if sw_ms >= bf_ms:
-        kernel, ms, n, b = "k_sweep", sw_ms, sw_n, sw_b
+        kernel, ms, n, units = "k_sweep", sw_ms, sw_n, sw_units
     else:
-        kernel, ms, n, b = "k_bf_round", bf_ms, bf_n, bf_b
+        kernel, ms, n, units = "k_bf_round", bf_ms, bf_n, bf_units
+    b = B_UNIT * units
     achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic = None
+    line = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "bytes_per_unit": B_UNIT, "units_per_launch": round(units / max(1, n), 1),
+            "bytes_per_launch": round(b / max(1, n), 1), "avg_launch_us": round(1e3 * ms / max(1, n), 3),
+            "launches": n, "kernel_ms_per_step": round(ms / n_res, 3),
+            "other_kernel": {"k_sweep": {"ms_per_step": round(sw_ms / n_res, 3), "launches": sw_n,
+                                         "units": sw_units},
+                             "k_bf_round": {"ms_per_step": round(bf_ms / n_res, 3), "launches": bf_n,
+                                            "units": bf_units}}}
+    if kernel == "k_bf_round":
+        a44 = B_RELAX * units / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        line["achieved_44B"] = round(a44, 3)
+        line["frac_44B"] = round(a44 / HBM_PEAK_GBS, 6)
     if os.path.exists(PMC_FILE):
         pmc = json.load(open(PMC_FILE))
-        traffic = pmc.get(kernel, {}).get("bytes_per_launch")
-    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "bytes_per_launch": round(b / max(1, n), 1), "avg_launch_us": round(1e3 * ms / max(1, n), 3),
-            "launches": n, "kernel_ms_per_step": round(ms / max(1, len(results)), 3),
-            "other_kernel": {"k_sweep": {"ms_per_step": round(sw_ms / max(1, len(results)), 3), "launches": sw_n,
-                                         "bytes": sw_b},
-                             "k_bf_round": {"ms_per_step": round(bf_ms / max(1, len(results)), 3), "launches": bf_n,
-                                            "bytes": bf_b}}}
+        k = pmc.get("kernels", {}).get(kernel, {})
+        line["traffic"] = k.get("raw_bytes_per_launch")
+        line["traffic_source"] = {"file": os.path.relpath(PMC_FILE, ROOT), "date": pmc.get("date"),
+                                  "workload": pmc.get("workload"),
+                                  "calibrated_bytes_per_launch": k.get("calibrated_bytes_per_launch"),
+                                  "atomics_per_launch": k.get("tcc_atomic_per_launch"),
+                                  "note": pmc.get("note")}
+    return line
 
 
 def timed_cpu(fn, reps: int = 5, warmup: int = 1, pin: bool = True):

@@ -1,13 +1,22 @@
 #!/bin/bash
-# PMC traffic passes only (FETCH_SIZE, WRITE_SIZE in separate runs).
+# PMC passes over one config-3 bench step, one rocprofv3 run per pass (FETCH_SIZE
+# and WRITE_SIZE cannot share a pass; TCC holds 4 counters, TA 2), then a
+# kernel-trace pass for the per-kernel device time. Usage: gpu_pmc.sh TAG
 set -o pipefail
 OUT=gpurun_out/${1:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT/pmc_fetch" -o run -- \
-    python -u bench.py --steps 1 --warmup 0 --cpu-baseline off > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" \
-    || { echo "pmc fetch failed"; tail -20 "$OUT/pmc_fetch.err"; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT/pmc_write" -o run -- \
-    python -u bench.py --steps 1 --warmup 0 --cpu-baseline off > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err" \
-    || { echo "pmc write failed"; tail -20 "$OUT/pmc_write.err"; exit 1; }
-python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffic.json" && cat "$OUT/pmc_traffic.json"
+run_pass() {   # name, rocprofv3 args...
+    local name=$1; shift
+    timeout -s KILL 120 rocprofv3 "$@" -f csv -d "$OUT/$name" -o run -- \
+        python -u bench.py --steps 1 --warmup 0 --cpu-baseline off > "$OUT/$name.json" 2> "$OUT/$name.err" \
+        || { echo "pass $name failed"; tail -20 "$OUT/$name.err"; exit 1; }
+}
+run_pass fetch --pmc FETCH_SIZE
+run_pass write --pmc WRITE_SIZE
+run_pass atom --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum
+run_pass ta --pmc TA_FLAT_ATOMIC_WAVEFRONTS_sum
+run_pass trace --kernel-trace --stats
+python tools/pmc_per_kernel.py "$OUT/fetch" "$OUT/write" "$OUT/atom" "$OUT/ta" > "$OUT/pmc_per_kernel.json"
+python tools/prof_summary.py "$OUT/trace" > "$OUT/kernel_stats.csv"
+echo ok

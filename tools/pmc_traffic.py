@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Build profiles/<tag>_pmc_traffic.json from gpu_pmc.sh's passes and the
+calibration run (gpu_calib.sh): per kernel, raw FETCH_SIZE + WRITE_SIZE bytes
+per launch, the calibrated range, and atomic request counts / rates.
+
+    python tools/pmc_traffic.py gpurun_out/<pmc tag> gpurun_out/<calib tag> DATE > profiles/r02_pmc_traffic.json
+"""
+import csv
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_per_kernel  # noqa: E402
+
+
+def per_kernel(dirs):
+    import io
+    from contextlib import redirect_stdout
+    buf = io.StringIO()
+    argv = sys.argv
+    sys.argv = ["x"] + dirs
+    with redirect_stdout(buf):
+        pmc_per_kernel.main()
+    sys.argv = argv
+    return json.loads(buf.getvalue())
+
+
+def main():
+    pmc, cal, date = sys.argv[1], sys.argv[2], sys.argv[3]
+    k = per_kernel([os.path.join(pmc, p) for p in ("fetch", "write", "atom", "ta")])
+    c = per_kernel([os.path.join(cal, "pmc_FETCH_SIZE"), os.path.join(cal, "pmc_WRITE_SIZE")])
+    known = json.load(open(os.path.join(cal, "calib_FETCH_SIZE.json")))
+    calib = {
+        "stream8_fetch_per_byte": c["k_stream8"]["FETCH_SIZE"] * 1024 / known["k_stream8"],
+        "stream4_fetch_per_byte": c["k_stream4"]["FETCH_SIZE"] * 1024 / known["k_stream4"],
+        "gather8_fetch_bytes_per_load": c["k_gather8"]["FETCH_SIZE"] * 1024 / known["k_gather8_loads"],
+        "store8_write_per_byte": c["k_store8"]["WRITE_SIZE"] * 1024 / known["k_store8"],
+        "atomic8_write_bytes_per_op": c["k_atomic8"]["WRITE_SIZE"] * 1024 / known["k_atomic8_ops"],
+    }
+    times = {}
+    stats = os.path.join(pmc, "kernel_stats.csv")
+    if os.path.exists(stats):
+        for r in csv.DictReader(open(stats)):
+            name = r.get("kernel") or r.get("Name") or ""
+            for key in ("k_sweep", "k_bf_round", "k_saturate"):
+                if key + "<" in name or key + "(" in name or name.endswith(key):
+                    times.setdefault(key, {"calls": 0, "total_us": 0.0})
+                    times[key]["calls"] += int(float(r.get("calls", 0)))
+                    times[key]["total_us"] += float(r.get("total_us", 0.0))
+    out = {"date": date, "workload": "config 3 (bench.py --steps 1 --warmup 0): one full solve",
+           "note": "raw = (FETCH_SIZE + WRITE_SIZE) per launch from separate rocprofv3 --pmc passes; gfx950 "
+                   "FETCH_SIZE tallies coalesced 4/8-B streams at 1/2 of their bytes and a random 8-B gather at "
+                   "64 B (tools/calib/calib_fetch.hip), so the calibrated range is [raw, 2*FETCH + WRITE]; "
+                   "WRITE_SIZE counts 32 B per 8-B atomic",
+           "calibration": {kk: round(v, 4) for kk, v in calib.items()}, "kernels": {}}
+    merged = {}
+    for name, v in k.items():
+        base = "k_bf_round" if name.startswith("k_bf_round") else name
+        m = merged.setdefault(base, {"dispatches": 0, "FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "TCC_ATOMIC_sum": 0.0,
+                                     "TCC_EA0_ATOMIC_sum": 0.0, "TA_FLAT_ATOMIC_WAVEFRONTS_sum": 0.0})
+        m["dispatches"] += int(v.get("dispatches", 0))
+        for ckey in ("FETCH_SIZE", "WRITE_SIZE", "TCC_ATOMIC_sum", "TCC_EA0_ATOMIC_sum",
+                     "TA_FLAT_ATOMIC_WAVEFRONTS_sum"):
+            m[ckey] += float(v.get(ckey, 0.0))
+            m[ckey + "_n"] = m.get(ckey + "_n", 0) + int(v.get(ckey + "_dispatches", 0))
+    for name, m in merged.items():
+        per = {c: m[c] / max(1, m.get(c + "_n", 0)) for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_ATOMIC_sum",
+                                                              "TCC_EA0_ATOMIC_sum", "TA_FLAT_ATOMIC_WAVEFRONTS_sum")}
+        fetch, write = per["FETCH_SIZE"] * 1024, per["WRITE_SIZE"] * 1024
+        rec = {"dispatches_per_pass": {c: m.get(c + "_n", 0) for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_ATOMIC_sum",
+                                                                       "TA_FLAT_ATOMIC_WAVEFRONTS_sum")},
+               "raw_fetch_bytes_per_launch": round(fetch, 1), "raw_write_bytes_per_launch": round(write, 1),
+               "raw_bytes_per_launch": round(fetch + write, 1),
+               "calibrated_bytes_per_launch": [round(fetch + write, 1), round(2 * fetch + write, 1)],
+               "tcc_atomic_per_launch": round(per["TCC_ATOMIC_sum"], 1),
+               "ea_atomic_per_launch": round(per["TCC_EA0_ATOMIC_sum"], 1),
+               "ta_flat_atomic_wavefronts_per_launch": round(per["TA_FLAT_ATOMIC_WAVEFRONTS_sum"], 1)}
+        t = times.get(name)
+        if t and t["total_us"] > 0:
+            rec["device_us_total"] = round(t["total_us"], 1)
+            rec["trace_calls"] = t["calls"]
+            rec["avg_launch_us"] = round(t["total_us"] / max(1, t["calls"]), 3)
+            # 64-bit atomics per second while the kernel runs: per-launch requests ÷ mean launch time
+            rec["tcc_atomics_per_s"] = round(per["TCC_ATOMIC_sum"] / (rec["avg_launch_us"] / 1e6), 1)
+        out["kernels"][name] = rec
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    main()
