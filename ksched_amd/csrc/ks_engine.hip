@@ -27,7 +27,7 @@
 //              ballots its flags, clears what it reads and hands the active
 //              nodes to its groups. Dense passes take every node.
 //   sweep      every frontier node discharges once against a price SNAPSHOT
-//              (double-buffered prices: read P[q], write P[q^1]); a node
+//              (double-buffered prices: read P[ni(q)], write P[ni(q^1)]); a node
 //              relabels only if it saturated all of its own admissible arcs, and
 //              the relabel also covers arcs that may gain residual capacity from
 //              concurrent pushes in the same sweep (reduced cost in (0, ε]) —
@@ -132,7 +132,7 @@ struct DG {
     const long long* ucap;   // rcap(a) + rcap(rev a), constant
     const long long* cost;
     long long* excess;
-    long long* p0;
+    long long* p0;         // node records (stride 4, index with ni()): p0 at +0, dist at +1, p1 at +2
     long long* p1;
     long long* dist;
     long long* inbox;
@@ -156,6 +156,10 @@ struct DG {
     unsigned long long* ctr;
     unsigned long long* stamps;   // diagnostic builds (-DKS_STAMPS): per launch [first start, last end|kind]
 };
+
+// Node records: p0, dist, p1 (and a pad) of a node share one 32-B record, so the
+// Bellman-Ford gathers of a tail's price and distance are one cache line.
+__host__ __device__ __forceinline__ size_t ni(long long x) { return 4 * (size_t)x; }
 
 // ---------------------------------------------------------------- atomics ---
 __device__ __forceinline__ void atom_add(long long* p, long long v) {
@@ -599,8 +603,8 @@ __global__ void k_reset_nodes(int nn, int ncap, const int* __restrict__ iperm, c
     for (long long x = blockIdx.x * (long long)BLK + threadIdx.x; x < nn; x += (long long)gridDim.x * BLK) {
         const int v = iperm[x];
         excess[x] = (v >= 0 && v < ncap && alive[v]) ? supply[v] : 0;
-        p0[x] = 0;
-        p1[x] = 0;
+        p0[ni(x)] = 0;
+        p1[ni(x)] = 0;
     }
 }
 
@@ -651,7 +655,7 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
     if (v >= 0) {
         b0 = g.first[v];
         en = g.first[v + 1];
-        pv = P[v];
+        pv = P[ni(v)];
     }
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;   // G == 64: one node per wave
     long long tot = 0;
@@ -661,7 +665,7 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
             const long long r = g.rcap[a];
             if (r > 0) {
                 const int w = g.head[a];
-                if (g.cost[a] + pv - P[w] < -thr) {
+                if (g.cost[a] + pv - P[ni(w)] < -thr) {
                     push_arc(g, nullptr, a, w, r, r, pd, out);
                     tot += r;
                     c.push++;
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
     if ((int)blockIdx.x < g.nhitems) {
         __shared__ long long sh[WPB];
         const HItem it = g.hitems[blockIdx.x];
-        const long long px = P[it.node];
+        const long long px = P[ni(it.node)];
         long long tot = 0;
 #pragma unroll
         for (int k = 0; k < PER_T; ++k) {
@@ -693,7 +697,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
                 const long long r = g.rcap[a];
                 if (r > 0) {
                     const int w = g.head[a];
-                    if (g.cost[a] + px - P[w] < -thr) {
+                    if (g.cost[a] + px - P[ni(w)] < -thr) {
                         push_arc(g, nullptr, a, w, r, r, pd, out);
                         tot += r;
                         c.push++;
@@ -741,7 +745,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
             w = g.head[a];
             rv = g.rev[a];     // issued with the arc: a push needs no further load
             uc = g.ucap[a];
-            cr = g.cost[a] + pv - P[w];
+            cr = g.cost[a] + pv - P[ni(w)];
             c.scan++;
         }
         const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
@@ -776,7 +780,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
             nf.flag[v] = 1;   // still active next sweep
             out = 1;
         }
-        PN[v] = np;
+        PN[ni(v)] = np;
     }
 }
 
@@ -826,7 +830,7 @@ __device__ __forceinline__ void settle(const DG& g, const Front& F, const Front&
         c.relabel++;
     }
     c.visit++;
-    PN[x] = np;
+    PN[ni(x)] = np;
     if (now > 0) mark(g, N, x, out);
     if (!hub) F.flag[x] = 0;   // every chunk has read it
     atom_exch_i(&g.q_arrive[slot], 0);
@@ -839,7 +843,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
     const int x = it.node;
-    const long long px = P[x];
+    const long long px = P[ni(x)];
     const long long E = atom_load(&g.excess[x]);
     long long r[PER_T], cr[PER_T], adm[PER_T], uc[PER_T];
     int w[PER_T], rv[PER_T];
@@ -863,7 +867,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
         const int a = it.begin + threadIdx.x * PER_T + k;
         cr[k] = 0;
         if (a < it.end) {
-            cr[k] = g.cost[a] + px - P[w[k]];
+            cr[k] = g.cost[a] + px - P[ni(w[k])];
             c.scan++;
         }
         adm[k] = (a < it.end && cr[k] < 0 && r[k] > 0) ? r[k] : 0;
@@ -915,7 +919,7 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
     if (lane == 0) F.flag[x] = 0;   // the lead consumes the node's flag
     const long long e = atom_load(&g.excess[x]);
     if (e <= 0) return;
-    const long long px = P[x];
+    const long long px = P[ni(x)];
     const int b0 = g.first[x], en = g.first[x + 1];
     if (lane == 0) c.visit++;
     long long rem = e, minc = INF64;
@@ -935,7 +939,7 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
             }
         }
 #pragma unroll
-        for (int j = 0; j < NB; ++j) pw[j] = (base + j * 64 + lane < en) ? P[w[j]] : 0;
+        for (int j = 0; j < NB; ++j) pw[j] = (base + j * 64 + lane < en) ? P[ni(w[j])] : 0;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const int a = base + j * 64 + lane;
@@ -978,7 +982,7 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
             N.flag[x] = 1;
             out = 1;
         }
-        PN[x] = np;
+        PN[ni(x)] = np;
     }
 }
 
@@ -1029,7 +1033,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         int b0 = 0, en = 0;
         if (v >= 0) {
             e = atom_load(&g.excess[v]);
-            pv = P[v];
+            pv = P[ni(v)];
             b0 = g.first[v];
             en = g.first[v + 1];
         }
@@ -1152,14 +1156,14 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
         const int h = u - g.hub_base;
         if (h < HUB_LDS) {
             __hip_atomic_fetch_min(&hub_min[h], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (cand < atom_min_ret(&g.dist[u], cand)) {
+        } else if (cand < atom_min_ret(&g.dist[ni(u)], cand)) {
             nf.hub[h] = 1;
             out = 1;
         }
         return false;
     }
     if (cand >= du) return false;
-    atom_min(&g.dist[u], cand);
+    atom_min(&g.dist[ni(u)], cand);
     return true;
 }
 
@@ -1178,8 +1182,8 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
     for (int b = b1 - b0 > 8 ? b0 + 8 : b1; b < b1; ++b)   // leaves have ≤ 8 arcs; kept for safety
         if (g.ucap[b] - g.rcap[b] > 0) {
             const int u2 = g.head[b];
-            const long long cand = du + arc_len<PR>(g.p0[u2], g.cost[b], pu, eps);
-            if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[u2] : INF64, hub_min, out)) {
+            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], g.cost[b], pu, eps);
+            if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
             }
@@ -1189,8 +1193,8 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         live &= live - 1;
         const int u2 = g.head[b];
         const long long cb = g.cost[b];
-        const long long pu2 = g.p0[u2];
-        const long long du2 = u2 < g.hub_base ? g.dist[u2] : INF64;
+        const long long pu2 = g.p0[ni(u2)];
+        const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
         const long long cand = du + arc_len<PR>(pu2, cb, pu, eps);
         if (offer<PR>(g, nf, u2, cand, du2, hub_min, out)) {
             nf.flag[u2] = 1;
@@ -1207,8 +1211,8 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     const long long rin = g.ucap[a] - g.rcap[a];
     const int u = g.head[a];
     const long long ca = g.cost[a];
-    const long long pu = g.p0[u];
-    const long long du = u < g.hub_base ? g.dist[u] : INF64;
+    const long long pu = g.p0[ni(u)];
+    const long long du = u < g.hub_base ? g.dist[ni(u)] : INF64;
     if (rin <= 0) return;
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
     if (!offer<PR>(g, nf, u, cand, du, hub_min, out)) return;
@@ -1252,8 +1256,8 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         long long d = INF64, pv = 0;
         int b0 = 0, en = 0;
         if (v >= 0) {
-            d = atom_load(&g.dist[v]);
-            pv = g.p0[v];
+            d = atom_load(&g.dist[ni(v)]);
+            pv = g.p0[ni(v)];
             b0 = g.first[v];
             en = g.first[v + 1];
         }
@@ -1266,11 +1270,11 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
 template <bool PR>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
                                          long long* hub_min, int& out, long long& scans) {
-    const long long dv = atom_load(&g.dist[ci.node]);
+    const long long dv = atom_load(&g.dist[ni(ci.node)]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
-        relax_in<PR>(g, N, a, dv, g.p0[ci.node], eps, hub_min, out);
+        relax_in<PR>(g, N, a, dv, g.p0[ni(ci.node)], eps, hub_min, out);
         scans++;
     }
 }
@@ -1280,12 +1284,12 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
     long long dv = INF64;
-    if (v >= 0) dv = atom_load(&g.dist[v]);
+    if (v >= 0) dv = atom_load(&g.dist[ni(v)]);
     const bool act = v >= 0 && (PR || dv < INF64);
     long long pv = 0;
     int b0 = 0, en = 0;
     if (act) {
-        pv = g.p0[v];
+        pv = g.p0[ni(v)];
         b0 = g.first[v];
         en = g.first[v + 1];
     }
@@ -1325,9 +1329,9 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     if ((int)blockIdx.x < g.nhitems) {
         const HItem it = g.hitems[blockIdx.x];
         if (dense || F.hub[it.hid]) {
-            const long long dv = atom_load(&g.dist[it.node]);
+            const long long dv = atom_load(&g.dist[ni(it.node)]);
             if (PR || dv < INF64) {
-                const long long pv = g.p0[it.node];
+                const long long pv = g.p0[ni(it.node)];
 #pragma unroll
                 for (int k = 0; k < PER_T; ++k) {
                     const int a = it.begin + threadIdx.x * PER_T + k;
@@ -1390,7 +1394,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
     if (threadIdx.x < HUB_LDS && (int)threadIdx.x < g.nheavy) {
         const long long val = hub_min[threadIdx.x];
         if (val < INF64) {
-            long long* dx = &g.dist[g.hub_base + threadIdx.x];
+            long long* dx = &g.dist[ni(g.hub_base + threadIdx.x)];
             if (val < atom_load(dx) && val < atom_min_ret(dx, val)) {
                 N.hub[threadIdx.x] = 1;
                 out = 1;
@@ -1439,7 +1443,7 @@ __global__ void k_gu_init(DG g) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         if (v >= g.hub_base) drain_inbox(g, (int)v - g.hub_base);
         const long long e = atom_load(&g.excess[v]);
-        g.dist[v] = e < 0 ? 0 : INF64;
+        g.dist[ni(v)] = e < 0 ? 0 : INF64;
     }
 }
 
@@ -1451,7 +1455,7 @@ __global__ void k_pr_init(DG g) {
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
-        g.dist[v] = 0;
+        g.dist[ni(v)] = 0;
 }
 
 // max finite distance (only once the update converged); cleans the sweep
@@ -1466,7 +1470,7 @@ __global__ void k_gu_max(DG g) {
     if (!g.ctl->bf_done) return;
     long long mx = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long d = atom_load(&g.dist[v]);
+        const long long d = atom_load(&g.dist[ni(v)]);
         if (d < INF64) mx = max(mx, d);
     }
     mx = wave_max(mx);
@@ -1490,13 +1494,13 @@ __global__ void k_gu_apply(DG g, int sseq) {
     const Front F = g.sf[sseq % 3];
     int out = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long d = atom_load(&g.dist[v]);
+        const long long d = atom_load(&g.dist[ni(v)]);
         const long long e = atom_load(&g.excess[v]);
         if (d >= INF64 && e > 0) atomicOr(&g.ctl->infeasible, 8);
         const long long dd = d < L ? d : L;
-        const long long np = g.p0[v] - eps * dd;
-        g.p0[v] = np;
-        g.p1[v] = np;
+        const long long np = g.p0[ni(v)] - eps * dd;
+        g.p0[ni(v)] = np;
+        g.p1[ni(v)] = np;
         if (e > 0) mark(g, F, (int)v, out);
     }
     if (__any(out) && lane_id() == 0) g.ctl->apply_act = 1;
@@ -1507,9 +1511,9 @@ __global__ void k_pr_apply(DG g) {
     if (!g.ctl->bf_done) return;
     const long long eps = g.ctl->eps;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long np = g.p0[v] - eps * atom_load(&g.dist[v]);
-        g.p0[v] = np;
-        g.p1[v] = np;
+        const long long np = g.p0[ni(v)] - eps * atom_load(&g.dist[ni(v)]);
+        g.p0[ni(v)] = np;
+        g.p1[ni(v)] = np;
     }
 }
 
@@ -1568,7 +1572,7 @@ __global__ void k_verify_opt(DG g, long long m2) {
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
         if (g.rcap[p] > 0) {
             const int t = g.head[g.rev[p]];
-            const long long cr = g.cost[p] + g.p0[t] - g.p0[g.head[p]];
+            const long long cr = g.cost[p] + g.p0[ni(t)] - g.p0[ni(g.head[p])];
             if (cr < -eps) bad = 1;
         }
     }
@@ -1619,7 +1623,7 @@ __global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive,
 __global__ void k_save_prices(int ncap, const int* __restrict__ perm, const long long* __restrict__ p0,
                               long long* __restrict__ pslot) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK)
-        pslot[v] = p0[perm[v]];
+        pslot[v] = p0[ni(perm[v])];
 }
 
 // Saved prices by node slot, rescaled when the cost multiplier changed.
@@ -1632,8 +1636,8 @@ __global__ void k_restore_prices(int ncap, int n_prev, long long mult_prev, long
             const long long q = pslot[v];
             p = mult == mult_prev ? q : (q / mult_prev) * mult + (q % mult_prev) * mult / mult_prev;
         }
-        p0[perm[v]] = p;
-        p1[perm[v]] = p;
+        p0[ni(perm[v])] = p;
+        p1[ni(perm[v])] = p;
     }
 }
 
@@ -1645,10 +1649,10 @@ __global__ void k_fresh_prices(int ncap, const unsigned char* __restrict__ fresh
         const int x = perm[v];
         long long best = -INF64;
         for (int a = g.first[x]; a < g.first[x + 1]; ++a)
-            if (g.rcap[a] > 0) best = max(best, g.p0[g.head[a]] - g.cost[a]);
+            if (g.rcap[a] > 0) best = max(best, g.p0[ni(g.head[a])] - g.cost[a]);
         if (best > -INF64) {
-            g.p0[x] = best;
-            g.p1[x] = best;
+            g.p0[ni(x)] = best;
+            g.p1[ni(x)] = best;
         }
     }
 }
@@ -1658,7 +1662,7 @@ __global__ void k_max_viol(DG g, long long m2) {
     long long mx = 0;
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
         if (g.rcap[p] > 0) {
-            const long long cr = g.cost[p] + g.p0[g.head[g.rev[p]]] - g.p0[g.head[p]];
+            const long long cr = g.cost[p] + g.p0[ni(g.head[g.rev[p]])] - g.p0[ni(g.head[p])];
             if (-cr > mx) mx = -cr;
         }
     }
@@ -1891,7 +1895,8 @@ struct EngineImpl {
     long long mult = 1;       // cost multiplier (ncap + 1)
     int64_t m2cap = 0;        // residual positions (Σ segment capacities)
     DBuf<int> first, head, rev, ent, used, perm, iperm;
-    DBuf<long long> rcap, ucap, scost, excess, p0, p1, dist;
+    DBuf<long long> rcap, ucap, scost, excess;
+    DBuf<long long> nd;            // node records [p0, dist, p1, pad] × nn
     DBuf<unsigned> keys_in, keys_out;
     DBuf<int> vals_in, vals_out, pos_of, deg, capv, capi, rs;
     DBuf<unsigned char> sort_tmp, cls;
@@ -1967,7 +1972,7 @@ struct EngineImpl {
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
         first.release(); head.release(); rev.release(); ent.release(); used.release(); perm.release(); iperm.release();
-        rcap.release(); ucap.release(); scost.release(); excess.release(); p0.release(); p1.release(); dist.release();
+        rcap.release(); ucap.release(); scost.release(); excess.release(); nd.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
@@ -2040,9 +2045,9 @@ struct EngineImpl {
         g.ucap = ucap.p;
         g.cost = scost.p;
         g.excess = excess.p;
-        g.p0 = p0.p;
-        g.p1 = p1.p;
-        g.dist = dist.p;
+        g.p0 = nd.p;
+        g.p1 = nd.p ? nd.p + 2 : nullptr;
+        g.dist = nd.p ? nd.p + 1 : nullptr;
         g.inbox = inbox.p;
         for (int c = 0; c <= NGC; ++c) {
             g.obeg[c] = obeg[c];
@@ -2391,9 +2396,7 @@ static int build(EngineImpl& s, std::string& err) {
     KS_CHECK(s.ucap.ensure(m2cap));
     KS_CHECK(s.scost.ensure(m2cap));
     KS_CHECK(s.excess.ensure(std::max(nn, 1)));
-    KS_CHECK(s.p0.ensure(std::max(nn, 1)));
-    KS_CHECK(s.p1.ensure(std::max(nn, 1)));
-    KS_CHECK(s.dist.ensure(std::max(nn, 1)));
+    KS_CHECK(s.nd.ensure(4 * (size_t)std::max(nn, 1)));
     if (m2c)
         hipLaunchKernelGGL(k_inert_all, dim3(grid_for(m2c)), dim3(BLK), 0, st, (long long)m2c, nn,
                            (const int*)s.first.p, s.head.p, s.rev.p, s.ent.p, s.rcap.p, s.ucap.p, s.scost.p);
@@ -2500,7 +2503,7 @@ static int cold_reset(EngineImpl& s, std::string& err) {
                            (const int*)s.ent.p, (const long long*)s.ucap.p, s.rcap.p);
     hipLaunchKernelGGL(k_reset_nodes, dim3(grid_for(s.nn)), dim3(BLK), 0, st, s.nn, (int)s.ncap,
                        (const int*)s.iperm.p, (const unsigned char*)s.n_alive.p, (const long long*)s.n_supply.p,
-                       s.excess.p, s.p0.p, s.p1.p);
+                       s.excess.p, s.nd.p, (s.nd.p + 2));
     if (hi)
         hipLaunchKernelGGL(k_reset_low, dim3(grid_for(hi)), dim3(BLK), 0, st, hi, (const unsigned char*)s.a_alive.p,
                            (const int*)s.a_src.p, (const int*)s.a_dst.p, (const int*)s.perm.p,
@@ -2898,7 +2901,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                    (const unsigned char*)s.a_alive.p, (const int*)s.fwd.p, (const int*)s.rev.p,
                                    (const long long*)s.rcap.p, s.saved_flows.p);
             hipLaunchKernelGGL(k_save_prices, dim3(grid_for(ncap_prev)), dim3(BLK), 0, st, (int)ncap_prev,
-                               (const int*)s.perm.p, (const long long*)s.p0.p, s.p_slot.p);
+                               (const int*)s.perm.p, (const long long*)s.nd.p, s.p_slot.p);
         }
         int rc = build(s, err);
         if (rc) return rc;
@@ -2913,7 +2916,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                    (const int*)s.perm.p, s.rcap.p, s.excess.p);
             hipLaunchKernelGGL(k_restore_prices, dim3(grid_for(s.ncap)), dim3(BLK), 0, st, (int)s.ncap,
                                (int)ncap_prev, mult_prev, s.mult, (const long long*)s.p_slot.p, (const int*)s.perm.p,
-                               s.p0.p, s.p1.p);
+                               s.nd.p, (s.nd.p + 2));
         }
     } else if (!use_warm) {
         int rc = cold_reset(s, err);
