@@ -157,9 +157,17 @@ struct DG {
     unsigned long long* stamps;   // diagnostic builds (-DKS_STAMPS): per launch [first start, last end|kind]
 };
 
-// Node records: p0, dist, p1 (and a pad) of a node share one 32-B record, so the
-// Bellman-Ford gathers of a tail's price and distance are one cache line.
+// Node records: p0, dist, p1 and the node's segment bounds (first[x], first[x+1]
+// packed) share one 32-B record, so a Bellman-Ford tail gather (price, distance,
+// and a leaf's segment) or a sweep's node load (price, segment) is one cache line.
 __host__ __device__ __forceinline__ size_t ni(long long x) { return 4 * (size_t)x; }
+constexpr int ND_SEG = 3;   // record slot of the packed segment bounds
+
+__device__ __forceinline__ void seg_of(const long long* nd, int x, int& b0, int& b1) {
+    const unsigned long long w = (unsigned long long)nd[ni(x) + ND_SEG];
+    b0 = (int)(unsigned)(w & 0xffffffffULL);
+    b1 = (int)(unsigned)(w >> 32);
+}
 
 // ---------------------------------------------------------------- atomics ---
 __device__ __forceinline__ void atom_add(long long* p, long long v) {
@@ -597,6 +605,12 @@ __global__ void k_reset_pos(long long m2cap, const int* __restrict__ ent, const 
     }
 }
 
+// Segment bounds into the node records (the CSR's first[] is fixed per build).
+__global__ void k_node_bounds(int nn, const int* __restrict__ first, long long* __restrict__ nd) {
+    for (long long x = blockIdx.x * (long long)BLK + threadIdx.x; x < nn; x += (long long)gridDim.x * BLK)
+        nd[ni(x) + ND_SEG] = (long long)(((unsigned long long)(unsigned)first[x + 1] << 32) | (unsigned)first[x]);
+}
+
 __global__ void k_reset_nodes(int nn, int ncap, const int* __restrict__ iperm, const unsigned char* __restrict__ alive,
                               const long long* __restrict__ supply, long long* __restrict__ excess,
                               long long* __restrict__ p0, long long* __restrict__ p1) {
@@ -653,8 +667,7 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
     int b0 = 0, en = 0;
     long long pv = 0;
     if (v >= 0) {
-        b0 = g.first[v];
-        en = g.first[v + 1];
+        seg_of(g.p0, v, b0, en);
         pv = P[ni(v)];
     }
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;   // G == 64: one node per wave
@@ -920,7 +933,8 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
     const long long e = atom_load(&g.excess[x]);
     if (e <= 0) return;
     const long long px = P[ni(x)];
-    const int b0 = g.first[x], en = g.first[x + 1];
+    int b0, en;
+    seg_of(g.p0, x, b0, en);
     if (lane == 0) c.visit++;
     long long rem = e, minc = INF64;
     for (int base = b0; base < en; base += 64 * NB) {
@@ -1034,8 +1048,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         if (v >= 0) {
             e = atom_load(&g.excess[v]);
             pv = P[ni(v)];
-            b0 = g.first[v];
-            en = g.first[v + 1];
+            seg_of(g.p0, v, b0, en);
         }
         sweep_group<G>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
@@ -1171,10 +1184,9 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 // its distance dropped to du: a second hop inside the same round.
 template <bool PR>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
-                                            long long eps, long long* hub_min, int& out) {
+                                            int b0, int b1, long long eps, long long* hub_min, int& out) {
     // residual tests of all (≤ 8) arcs issued together; usually one in-arc carries
     // flow (a task's assignment), so the dependent loads follow for it alone
-    const int b0 = g.first[u], b1 = g.first[u + 1];
     unsigned live = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -1213,11 +1225,14 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     const long long ca = g.cost[a];
     const long long pu = g.p0[ni(u)];
     const long long du = u < g.hub_base ? g.dist[ni(u)] : INF64;
+    const bool leaf = g.expand && u < g.obeg[2];
+    int b0 = 0, b1 = 0;
+    if (leaf) seg_of(g.p0, u, b0, b1);   // same record line as pu, du
     if (rin <= 0) return;
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
     if (!offer<PR>(g, nf, u, cand, du, hub_min, out)) return;
-    if (g.expand && u < g.obeg[2]) {
-        expand_leaf<PR>(g, nf, u, cand, pu, eps, hub_min, out);   // tasks, PUs: two hops per round
+    if (leaf) {
+        expand_leaf<PR>(g, nf, u, cand, pu, b0, b1, eps, hub_min, out);   // tasks, PUs: two hops per round
     } else {
         nf.flag[u] = 1;
         out = 1;
@@ -1258,8 +1273,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         if (v >= 0) {
             d = atom_load(&g.dist[ni(v)]);
             pv = g.p0[ni(v)];
-            b0 = g.first[v];
-            en = g.first[v + 1];
+            seg_of(g.p0, v, b0, en);
         }
         bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, hub_min, out, scans);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
@@ -1290,8 +1304,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
     int b0 = 0, en = 0;
     if (act) {
         pv = g.p0[ni(v)];
-        b0 = g.first[v];
-        en = g.first[v + 1];
+        seg_of(g.p0, v, b0, en);
     }
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
     for (int it = 0; it < iters; ++it) {
@@ -2397,6 +2410,8 @@ static int build(EngineImpl& s, std::string& err) {
     KS_CHECK(s.scost.ensure(m2cap));
     KS_CHECK(s.excess.ensure(std::max(nn, 1)));
     KS_CHECK(s.nd.ensure(4 * (size_t)std::max(nn, 1)));
+    if (nn)
+        hipLaunchKernelGGL(k_node_bounds, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, (const int*)s.first.p, s.nd.p);
     if (m2c)
         hipLaunchKernelGGL(k_inert_all, dim3(grid_for(m2c)), dim3(BLK), 0, st, (long long)m2c, nn,
                            (const int*)s.first.p, s.head.p, s.rev.p, s.ent.p, s.rcap.p, s.ucap.p, s.scost.p);
