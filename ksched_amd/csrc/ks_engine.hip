@@ -73,6 +73,9 @@ constexpr int PER_T = CHUNK / 256; // arcs per thread in a hub chunk
 #define KS_WPW 2
 #endif
 constexpr int WPW = KS_WPW;        // windows per wave in sparse (grid-stride) passes
+#ifndef KS_NB
+#define KS_NB 4                    // chunked-node discharge: 64-arc batches in flight per wave
+#endif
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -144,6 +147,8 @@ struct DG {
     int nheavy;
     const CItem* citems;   // chunks of the chunked class
     int ncitems;
+    int ncls_c;            // nodes of the chunked class
+    int sw_clsb;           // sweep blocks striding the class windows (after the hub blocks)
     const int* hnchunks;
     long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
     long long* q_taken;
@@ -938,18 +943,22 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
     if (lane == 0) c.visit++;
     long long rem = e, minc = INF64;
     for (int base = b0; base < en; base += 64 * NB) {
-        long long r[NB], cs[NB], pw[NB];
-        int w[NB];
+        long long r[NB], cs[NB], pw[NB], uc[NB];
+        int w[NB], rv[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const int a = base + j * 64 + lane;
             r[j] = 0;
             cs[j] = 0;
             w[j] = 0;
-            if (a < en) {
+            rv[j] = 0;
+            uc[j] = 0;
+            if (a < en) {   // reverse position and pair capacity too: a push needs no further load
                 r[j] = g.rcap[a];
                 w[j] = g.head[a];
                 cs[j] = g.cost[a];
+                rv[j] = g.rev[a];
+                uc[j] = g.ucap[a];
             }
         }
 #pragma unroll
@@ -967,7 +976,7 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
                 d = rem - (incl - adm);
                 d = d < 0 ? 0 : (d > adm ? adm : d);
                 if (d > 0) {
-                    push_arc(g, &N, a, w[j], r[j], d, pd, out);
+                    push_arc(g, &N, a, w[j], r[j], d, pd, out, rv[j], uc[j]);
                     c.push++;
                 }
                 rem -= total < rem ? total : rem;
@@ -1100,24 +1109,32 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             kind = 1;
 #endif
         }
+    } else if ((int)blockIdx.x >= g.nhitems + g.sw_clsb) {
+        // chunked class: one wave per node, so no wave serialises two of them
+        const int i = ((int)blockIdx.x - g.nhitems - g.sw_clsb) * WPB + (int)(threadIdx.x >> 6);
+        if (i < g.ncls_c) {
+            const int x = g.obeg[CCLS] + i;
+            if (F.flag[x]) {
+                node_discharge<KS_NB>(g, F, N, x, P, PN, eps, pd, out, c);
+#ifdef KS_STAMPS
+                kind = 2;
+#endif
+            }
+        }
     } else {
-        const int tw = ((int)gridDim.x - g.nhitems) * WPB;
+        // class windows, WPW per wave strided across the class blocks
+        const int tw = g.sw_clsb * WPB;
         const int w0 = wave_index_in_grid(g.nhitems);
         unsigned long long mk[WPW];
 #pragma unroll
-        for (int j = 0; j < WPW; ++j) mk[j] = window_mask(g, F.flag, w0 + j * tw, true);
+        for (int j = 0; j < WPW; ++j) {
+            const int w = w0 + j * tw;
+            mk[j] = w < g.wbeg[CCLS] ? window_mask(g, F.flag, w, true) : 0;
+        }
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
-            if (w >= g.wbeg[CCLS]) {
-                const CItem ci = g.citems[w - g.wbeg[CCLS]];
-                if (ci.lead) node_discharge<8>(g, F, N, ci.node, P, PN, eps, pd, out, c);
-#ifdef KS_STAMPS
-                kind = max(kind, 2);
-#endif
-                continue;
-            }
 #ifdef KS_STAMPS
             kind = max(kind, 3 + class_of_window(g, w));
 #endif
@@ -2071,6 +2088,8 @@ struct EngineImpl {
         g.nhitems = nhitems;
         g.citems = citems.p;
         g.ncitems = ncitems;
+        g.ncls_c = ncls[CCLS];
+        g.sw_clsb = sweep_cls_blocks();
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
         g.q_req = q_req.p;
@@ -2092,6 +2111,9 @@ struct EngineImpl {
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
     int dense_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
+    int sweep_cls_blocks() const { return std::max(1, (wbeg[CCLS] + WPW * WPB - 1) / (WPW * WPB)); }
+    // sweeps: hub chunks, class-window blocks, one wave per chunked-class node
+    int sweep_grid() const { return nhitems + sweep_cls_blocks() + (ncls[CCLS] + WPB - 1) / WPB; }
     int sparse_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB)); }
     int hi() const { return h_sctl->hi; }
 };
@@ -2982,7 +3004,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     }
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
-    const int sgrid = s.sparse_grid();     // sparse sweeps and Bellman-Ford rounds
+    const int sgrid = s.sparse_grid();     // sparse Bellman-Ford rounds
+    const int wgrid = s.sweep_grid();      // sweeps
     const int ngrid = grid_for(nn, 2048);
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi_base = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
@@ -3091,7 +3114,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             KS_CHECK(hipEventRecord(s.kev[2], st));
-            for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(sgrid), dim3(BLK), 0, st, g, k, sseq + k);
+            for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             KS_CHECK(hipEventRecord(s.kev[3], st));
             KS_CHECK(read_ctl());
             sweep_kernels += gi;
