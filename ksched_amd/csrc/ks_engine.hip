@@ -79,6 +79,7 @@ constexpr int WPW = KS_WPW;        // windows per wave in sparse (grid-stride) p
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
+constexpr int CYC_SLOTS = 2;       // control snapshots / timing events rotate over two cycles
 constexpr int NCTR = 8;
 constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
@@ -97,6 +98,9 @@ struct Ctl {
     int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
     int apply_act;         // the global-update apply seeded a non-empty frontier
     int sweep_act[MAXB];   // sweep pos left a non-empty frontier
+    int gu_pending;        // the last cycle's update did not converge: the next cycle continues it
+    int bf_r0;             // bf_count when the running update started
+    int bf_seq0;           // sequence number of the running update's first (dense) round
 };
 
 struct HItem {
@@ -1334,8 +1338,11 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
 }
 
 // One Bellman-Ford round. dense = 1: every node (first round of an update).
+// dense_arg < 0: the round is dense iff it is the running update's first
+// (bf_seq0, set by the init kernel); ≥ 0: as given.
 template <bool PR>
-__global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense) {
+__global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) {
+    const int dense = dense_arg >= 0 ? dense_arg : (seq == g.ctl->bf_seq0 ? 1 : 0);
     __shared__ long long hub_min[HUB_LDS];
     if (blockIdx.x == 0) {
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.bf[(seq + 2) % 3].hub[h] = 0;
@@ -1463,11 +1470,16 @@ __device__ __forceinline__ void clear_fronts(const DG& g, const Front* fs) {
 }
 
 // GU init: drain hub inboxes, dist = 0 at deficits / INF elsewhere, clean flags.
-__global__ void k_gu_init(DG g) {
+// A cycle whose predecessor left its update unconverged (gu_pending) continues
+// that update instead; seq0 = the sequence number of this cycle's first round.
+__global__ void k_gu_init(DG g, int seq0) {
+    if (g.ctl->gu_pending) return;
     clear_fronts(g, g.bf);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
         g.ctl->gu_L = 0;
+        g.ctl->bf_r0 = g.ctl->bf_count;
+        g.ctl->bf_seq0 = seq0;
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
@@ -1478,14 +1490,29 @@ __global__ void k_gu_init(DG g) {
 }
 
 // PR init: dist = 0 everywhere.
-__global__ void k_pr_init(DG g) {
+__global__ void k_pr_init(DG g, int seq0) {
     clear_fronts(g, g.bf);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
+        g.ctl->bf_seq0 = seq0;
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
         g.dist[ni(v)] = 0;
+}
+
+// End of a cycle: an update that has not converged is continued by the next
+// cycle; the control block goes straight to pinned host memory (a copy engine
+// transfer would drain the queue around it: ~65 µs of idle GPU per cycle).
+__global__ void k_cycle_end(DG g, Ctl* host) {
+    static_assert(sizeof(Ctl) % 4 == 0, "Ctl is copied as words");
+    if (threadIdx.x == 0) g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;
+    __syncthreads();
+    const int* src = reinterpret_cast<const int*>(g.ctl);
+    int* dst = reinterpret_cast<int*>(host);
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x)
+        __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
 }
 
 // max finite distance (only once the update converged); cleans the sweep
@@ -1893,7 +1920,12 @@ struct EngineImpl {
     ks_opts opts{};
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
-    hipEvent_t kev[4] = {};   // per-cycle kernel-batch timing: BF rounds, sweeps
+    hipEvent_t kev[4] = {};   // kernel-batch timing (price refinement)
+    hipEvent_t cev[CYC_SLOTS][2] = {};  // per-cycle timing: after the BF rounds, after the apply
+    hipEvent_t cdone[CYC_SLOTS] = {};   // a cycle's control snapshot has landed (timed: cycle end)
+    hipEvent_t cstart = nullptr;        // start of a phase's first cycle
+    Ctl* h_cyc[CYC_SLOTS] = {};         // pinned control snapshots of the cycles in flight
+    Ctl* d_cyc[CYC_SLOTS] = {};         // their device-side addresses (written by k_cycle_end)
 
     // ---- node store (by slot = id − 1)
     int64_t nstore = 0;       // allocated slots
@@ -2013,6 +2045,14 @@ struct EngineImpl {
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
+        for (auto* h : h_cyc)
+            if (h) (void)hipHostFree(h);
+        for (auto& c : cev)
+            for (auto& e : c)
+                if (e) (void)hipEventDestroy(e);
+        for (auto& e : cdone)
+            if (e) (void)hipEventDestroy(e);
+        if (cstart) (void)hipEventDestroy(cstart);
         if (h_scr) (void)hipHostFree(h_scr);
         if (h_sctl) (void)hipHostFree(h_sctl);
         for (auto& e : ev)
@@ -2145,6 +2185,15 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     KS_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
     for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
+    for (auto& c : s.cev)
+        for (auto& e : c) KS_CHECK(hipEventCreate(&e));
+    for (auto& e : s.cdone) KS_CHECK(hipEventCreate(&e));
+    KS_CHECK(hipEventCreate(&s.cstart));
+    for (int i = 0; i < CYC_SLOTS; ++i) {
+        KS_CHECK(hipHostMalloc(&s.h_cyc[i], sizeof(Ctl), hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(s.h_cyc[i], 0, sizeof(Ctl));
+        KS_CHECK(hipHostGetDevicePointer((void**)&s.d_cyc[i], s.h_cyc[i], 0));
+    }
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
     KS_CHECK(s.sctl.ensure(1));
@@ -3047,7 +3096,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     auto price_refine = [&](long long eps_try, int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(set_eps(eps_try));
-        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g);
+        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
         int used = 0, ok = 0;
         for (int batch = 0; used < cap; ++batch) {
             const int k = std::min(64, cap - used);
@@ -3097,63 +3146,77 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipEventRecord(s.ev[2], st));
         hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 && use_warm ? warm_thr : 0LL);
         KS_CHECK(hipEventRecord(s.ev[3], st));
-        bool gu_running = false;
         uint64_t phase_sweeps = 0;
         const int gi = gi_base;
-        int gu_r0 = 0;   // bf_count when the running update started
-        for (;;) {
-            // one cycle: [GU init] [kb BF rounds] [max] [apply] [gi sweeps]
-            const bool new_gu = !gu_running;
-            if (new_gu) {
-                gu_r0 = s.h_ctl->bf_count;
-                hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g);
+        // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
+        // [apply][gi sweeps][end: control block → pinned host memory].
+        auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
+            hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+            for (int r = 0; r < kb; ++r) {   // the first round may be the update's dense one
+                hipLaunchKernelGGL(k_bf_round<false>, dim3(r == 0 ? dgrid : sgrid), dim3(BLK), 0, st, g, bseq, -1);
+                ++bseq;
+                ++bf_launches;
             }
-            KS_CHECK(hipEventRecord(s.kev[0], st));
-            bf_rounds(false, kb, new_gu);
-            KS_CHECK(hipEventRecord(s.kev[1], st));
+            hipError_t e = hipEventRecord(s.cev[par][0], st);
+            if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
-            KS_CHECK(hipEventRecord(s.kev[2], st));
+            if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
-            KS_CHECK(hipEventRecord(s.kev[3], st));
-            KS_CHECK(read_ctl());
+            hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
+            sseq += gi;
+            return hipEventRecord(s.cdone[par], st);
+        };
+        // Cycles run one at a time (enqueueing the next one before reading this
+        // one's control block was measured slower: the speculative launches cost
+        // more GPU time than the host's decision gap). Timing: BF = from the
+        // previous cycle's end (or the phase start) to after the BF rounds; sweeps
+        // = from after the apply to the cycle's end.
+        KS_CHECK(hipEventRecord(s.cstart, st));
+        hipEvent_t prev_end = s.cstart;
+        int cur = 0;
+        for (;;) {
+            KS_CHECK(enqueue(cur));
+            KS_CHECK(hipEventSynchronize(s.cdone[cur]));
+            const Ctl* hc = s.h_cyc[cur];
             sweep_kernels += gi;
-            ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
-            ms_sw_k += ev_ms(s.kev[2], s.kev[3]);
-            if (s.h_ctl->infeasible) {
+            const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][1], s.cdone[cur]);
+            ms_bf_k += t_bf;   // init + BF rounds
+            ms_sw_k += t_sw;   // sweeps + cycle end
+            prev_end = s.cdone[cur];
+            if (hc->infeasible) {
                 status = KS_E_INFEASIBLE;
+                std::memcpy(s.h_ctl, hc, sizeof(Ctl));
                 break;
             }
-            if (!s.h_ctl->bf_done) {
-                // update still running: sweeps were skipped, keep relaxing
-                gu_running = true;
+            if (!hc->bf_done) {
+                // update still running: its sweeps were skipped and the next cycle continues it
                 kb = std::min(256, kb * 2);
-                sseq += gi;
+                cur ^= 1;
                 continue;
             }
-            gu_running = false;
             if (cycle_log)
                 std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d\n", phases, eps,
-                             s.h_ctl->bf_count - gu_r0, ev_ms(s.kev[0], s.kev[1]), ev_ms(s.kev[2], s.kev[3]),
-                             s.h_ctl->sweep_act[gi - 1]);
-            kb = std::max(8, std::min(256, s.h_ctl->bf_count - gu_r0 + 6));
+                             hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1]);
+            kb = std::max(8, std::min(256, hc->bf_count - hc->bf_r0 + 6));
             ++gus;
             sweeps += gi;
             sweep_launches += gi;
-            sseq += gi;
             phase_sweeps += gi;
             int last = 0;
             for (int k = 0; k < gi; ++k)
-                if (s.h_ctl->sweep_act[k]) last = k + 1;
-            if (!s.h_ctl->sweep_act[gi - 1]) {
+                if (hc->sweep_act[k]) last = k + 1;
+            if (!hc->sweep_act[gi - 1]) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
             }
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
+                (void)hipStreamSynchronize(st);
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
                       std::to_string(wall_s()) + " s)";
                 return KS_E_DEVICE;
             }
+            cur ^= 1;
         }
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
