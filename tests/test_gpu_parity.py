@@ -239,3 +239,38 @@ def test_out_of_range_update_is_rejected_without_side_effects(ctx):
     assert ei.value.code == native.KS_E_RANGE
     r = ctx.solve()
     assert (r.cost, r.flow) == (4, 1)      # 1→5→3 still there
+
+
+def test_mapping_with_flow_cycles_terminates_and_respects_pus(ctx):
+    """Task → PU decomposition on graphs whose optimal flow may run round
+    zero-cost cycles between intermediate nodes (ksched's own graphs are DAGs;
+    DESIGN §8 item 1): it must terminate, map only tasks to PUs, and keep every
+    PU within its PU → sink capacity."""
+    rng = np.random.default_rng(2024)
+    for trial in range(6):
+        T, K, P = 40, 12, 8                       # tasks, intermediate nodes, PUs
+        sink = 1
+        inter = list(range(2, 2 + K))
+        pus = list(range(2 + K, 2 + K + P))
+        tasks = list(range(2 + K + P, 2 + K + P + T))
+        nodes = [(sink, -T, 3)] + [(v, 0, 0) for v in inter] + [(p, 0, 2) for p in pus] + [(t, 1, 1) for t in tasks]
+        arcs = {}
+        for t in tasks:                            # each task: two intermediates and the sink (unscheduled)
+            for v in rng.choice(inter, 2, replace=False).tolist():
+                arcs[(t, v)] = (0, 1, int(rng.integers(1, 20)))
+            arcs[(t, sink)] = (0, 1, 200)
+        for _ in range(3 * K):                     # zero-cost arcs among intermediates (cycles)
+            a, b = rng.choice(inter, 2, replace=False).tolist()
+            arcs[(a, b)] = (0, int(rng.integers(1, 6)), 0)
+        for v in inter:
+            for p in rng.choice(pus, 2, replace=False).tolist():
+                arcs[(v, p)] = (0, int(rng.integers(1, 8)), int(rng.integers(0, 5)))
+        for p in pus:
+            arcs[(p, sink)] = (0, 4, 0)
+        g = graph_from_lists(nodes, [(s, d, lo, c, w) for (s, d), (lo, c, w) in arcs.items()])
+        st, cost, fv, _, _ = ko.ssp(g)
+        assert st == 0
+        ctx.load_graph(g)
+        r = ctx.solve()
+        assert (r.cost, r.flow) == (cost, fv), trial
+        check_mapping(g, ctx.task_mapping())
