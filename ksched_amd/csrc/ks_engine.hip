@@ -99,6 +99,7 @@ struct Ctl {
     int apply_act;         // the global-update apply seeded a non-empty frontier
     int sweep_act[MAXB];   // sweep pos left a non-empty frontier
     int gu_pending;        // the last cycle's update did not converge: the next cycle continues it
+    int n_exc;             // nodes the last apply found holding excess
     int bf_r0;             // bf_count when the running update started
     int bf_seq0;           // sequence number of the running update's first (dense) round
 };
@@ -1480,6 +1481,7 @@ __global__ void k_gu_init(DG g, int seq0) {
         g.ctl->gu_L = 0;
         g.ctl->bf_r0 = g.ctl->bf_count;
         g.ctl->bf_seq0 = seq0;
+        g.ctl->n_exc = 0;
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
@@ -1560,7 +1562,11 @@ __global__ void k_gu_apply(DG g, int sseq) {
         g.p1[ni(v)] = np;
         if (e > 0) mark(g, F, (int)v, out);
     }
-    if (__any(out) && lane_id() == 0) g.ctl->apply_act = 1;
+    const unsigned long long ex = __ballot(out);
+    if (ex && lane_id() == 0) {
+        g.ctl->apply_act = 1;
+        atomicAdd(&g.ctl->n_exc, (int)__popcll(ex));
+    }
 }
 
 // PR success: p ← p − ε·d (d ≤ 0).
@@ -3064,8 +3070,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
     const bool cycle_log = std::getenv("KS_CYCLE_LOG") != nullptr;   // diagnostic: one stderr line per cycle
+    // A phase that another phase follows may end with a few excess nodes left:
+    // refine's start (saturate every negative reduced cost) accepts any
+    // pseudoflow, so the next, finer phase absorbs them with its own excess.
+    // Only the last phase (the one price refinement may certify, or ε = 1) must
+    // end with a feasible flow. phase_exit = 0 disables the early end.
+    int phase_exit = 256;
+    if (const char* pe = std::getenv("KS_PHASE_EXIT")) phase_exit = std::max(0, std::atoi(pe));
     long long eps = std::max<long long>(1, maxc * mult);
-    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0;
+    uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0, early_exits = 0;
     double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
     int phases = 0;
     int kb = 24;                        // Bellman-Ford rounds enqueued per cycle (adaptive)
@@ -3210,6 +3223,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
             }
+            const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
+            if (!last_phase && hc->n_exc <= phase_exit) {
+                ++early_exits;
+                break;   // a coarse phase: the next one absorbs the few units left
+            }
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
@@ -3233,6 +3251,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
     } while (eps > 1);
 
+    if (cycle_log)
+        std::fprintf(stderr, "solve phases %d updates %llu early phase ends %llu\n", phases, (unsigned long long)gus,
+                     (unsigned long long)early_exits);
     if (status == KS_E_INFEASIBLE)
         err = "infeasible: some supply cannot reach a demand node (code " + std::to_string(s.h_ctl->infeasible) +
               ", phase " + std::to_string(phases) + ", eps " + std::to_string(eps) + ", updates " +
