@@ -3074,9 +3074,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // refine's start (saturate every negative reduced cost) accepts any
     // pseudoflow, so the next, finer phase absorbs them with its own excess.
     // Only the last phase (the one price refinement may certify, or ε = 1) must
-    // end with a feasible flow. phase_exit = 0 disables the early end.
-    int phase_exit = 256;
+    // end with a feasible flow. A coarse phase ends once at most phase_exit
+    // nodes AND at most 1/phase_frac of its peak hold excess (the relative bound
+    // keeps phases that start small — incremental rounds — doing their share).
+    // phase_exit = 0 disables the early end.
+    int phase_exit = 256, phase_frac = 128;
     if (const char* pe = std::getenv("KS_PHASE_EXIT")) phase_exit = std::max(0, std::atoi(pe));
+    if (const char* pf = std::getenv("KS_PHASE_FRAC")) phase_frac = std::max(1, std::atoi(pf));
     long long eps = std::max<long long>(1, maxc * mult);
     uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0, early_exits = 0;
     double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
@@ -3161,6 +3165,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipEventRecord(s.ev[3], st));
         uint64_t phase_sweeps = 0;
         const int gi = gi_base;
+        int phase_peak = 0;   // most excess nodes seen by an update of this phase
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][gi sweeps][end: control block → pinned host memory].
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
@@ -3224,7 +3229,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 break;   // no excess left: refine done
             }
             const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
-            if (!last_phase && hc->n_exc <= phase_exit) {
+            phase_peak = std::max(phase_peak, hc->n_exc);
+            if (!last_phase && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
