@@ -69,6 +69,12 @@ constexpr int NGC = 6;             // group classes: 4, 8, 16, 32, 64 lanes; 64 
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
 constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
 constexpr int PER_T = CHUNK / 256; // arcs per thread in a hub chunk
+#ifndef KS_HSPLIT
+#define KS_HSPLIT 4                // Bellman-Ford: workgroups per hub chunk (one arc per thread at 4)
+#endif
+constexpr int HSPLIT = KS_HSPLIT;
+constexpr int BF_PER_T = PER_T / HSPLIT;
+static_assert(PER_T % HSPLIT == 0, "a hub chunk splits into whole arcs per thread");
 #ifndef KS_WPW
 #define KS_WPW 2
 #endif
@@ -860,14 +866,13 @@ __device__ __forceinline__ void settle(const DG& g, const Front& F, const Front&
 }
 
 // Hub chunk: one workgroup, 1024 arcs (four per thread, loads issued together).
-__device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HItem& it,
+// px, E: the hub's price and excess, loaded by the caller with its flag.
+__device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HItem& it, long long px, long long E,
                           const long long* __restrict__ P, long long* __restrict__ PN, long long eps, Pend& pd,
                           int& out, Cnt& c) {
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
     const int x = it.node;
-    const long long px = P[ni(x)];
-    const long long E = atom_load(&g.excess[x]);
     long long r[PER_T], cr[PER_T], adm[PER_T], uc[PER_T];
     int w[PER_T], rv[PER_T];
     long long mine = 0;
@@ -934,17 +939,15 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
 // batch issued together, then the price gathers), distributes the excess with
 // one wave scan per 64 arcs and relabels like sweep_group. One dependent chain
 // per batch instead of the claim/arrive protocol of hubs.
+// e, px, b0, en: the node's excess, price and segment, loaded by the caller
+// together with its frontier flag (one dependent step fewer).
 template <int NB>
-__device__ void node_discharge(const DG& g, const Front& F, const Front& N, int x,
-                               const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
-                               Pend& pd, int& out, Cnt& c) {
+__device__ void node_discharge(const DG& g, const Front& F, const Front& N, int x, long long e, long long px,
+                               int b0, int en, long long* __restrict__ PN, const long long* __restrict__ P,
+                               long long eps, Pend& pd, int& out, Cnt& c) {
     const int lane = lane_id();
     if (lane == 0) F.flag[x] = 0;   // the lead consumes the node's flag
-    const long long e = atom_load(&g.excess[x]);
     if (e <= 0) return;
-    const long long px = P[ni(x)];
-    int b0, en;
-    seg_of(g.p0, x, b0, en);
     if (lane == 0) c.visit++;
     long long rem = e, minc = INF64;
     for (int base = b0; base < en; base += 64 * NB) {
@@ -1025,24 +1028,49 @@ __device__ __forceinline__ int class_of_window(const DG& g, int w) {
     return c;
 }
 
-// Ballot of window w's flags. Class windows clear what they read (if clear);
-// chunk items only read (their node's flag is cleared by the node's owner).
-__device__ __forceinline__ unsigned long long window_mask(const DG& g, unsigned char* flags, int w, bool clear) {
-    bool on = false;
+// Window w's frontier flags in two steps, so a launch can issue them before it
+// knows whether it has work: window_load reads this lane's flag (class windows:
+// one node slot per lane; chunk items: the node's flag on lane 0), window_take
+// clears what was set (class windows only; a chunk item's flag is cleared by
+// the node's owner) and ballots it — nothing when go is false.
+struct WinFlag {
+    int slot;   // flag index this lane read (-1: none)
+    int raw;    // the flag byte
+};
+__device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char* flags, int w) {
+    w = __builtin_amdgcn_readfirstlane(w);   // wave-uniform: the class selection stays scalar
+    WinFlag f{-1, 0};
     const int ln = lane_id();
     if (w < g.wbeg[CCLS]) {
-        const int c = class_of_window(g, w);
-        const int ws = c < 4 ? (32 >> c) : 1;
-        const int slot = g.obeg[c] + (w - g.wbeg[c]) * ws + ln;
-        if (ln < ws) {
-            on = flags[slot] != 0;
-            if (on && clear) flags[slot] = 0;
-        }
+        // class c = the last with wbeg[c] <= w, selected over static fields (kernel
+        // arguments: no dependent load before the flag's)
+        int ob = g.obeg[0], wb = g.wbeg[0], ws = win_slots(0);
+#pragma unroll
+        for (int k = 1; k < CCLS; ++k)
+            if (w >= g.wbeg[k]) {
+                ob = g.obeg[k];
+                wb = g.wbeg[k];
+                ws = win_slots(k);
+            }
+        if (ln < ws) f.slot = ob + (w - wb) * ws + ln;
     } else if (w < g.wbeg[CCLS] + g.ncitems) {
-        if (ln == 0) on = flags[g.citems[w - g.wbeg[CCLS]].node] != 0;
+        if (ln == 0) f.slot = g.citems[w - g.wbeg[CCLS]].node;
     }
+    if (f.slot >= 0) f.raw = flags[f.slot];
+    return f;
+}
+__device__ __forceinline__ unsigned long long window_take(const DG& g, unsigned char* flags, int w, const WinFlag& f,
+                                                          bool go) {
+    const bool on = go && f.raw != 0;
+    if (on && w < g.wbeg[CCLS]) flags[f.slot] = 0;
     return __ballot(on);
 }
+
+// The control words of a launch pass through an empty asm that also takes the
+// launch's first loads as inputs: the words are only tested after every one of
+// those loads was issued (one wait for all of them; the compiler would
+// otherwise test the words first, or sink the other loads under the test).
+#define KS_AFTER_LOADS(c0, c1, ...) asm volatile("" : "+v"(c0), "+v"(c1) : __VA_ARGS__)
 
 template <int C>
 __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, unsigned long long mask,
@@ -1093,8 +1121,15 @@ __device__ __forceinline__ void stamp(const DG& g, int id, unsigned long long t0
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
-    if (!g.ctl->bf_done) return;   // the preceding global update has not been applied
-    if (!(pos == 0 ? g.ctl->apply_act : g.ctl->sweep_act[pos - 1])) return;   // empty frontier
+    // The preceding global update was applied (c_done) and the frontier is
+    // non-empty (c_act): tested only after each block issued its own first loads
+    // (flags, excess, node records; KS_AFTER_LOADS), so the control read is not
+    // a dependent step of its own.
+    int c_done, c_act;   // read in each branch, after its first loads
+    auto ctl_words = [&]() {
+        c_done = g.ctl->bf_done;
+        c_act = pos == 0 ? g.ctl->apply_act : g.ctl->sweep_act[pos - 1];
+    };
 #ifdef KS_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
     int kind = 0;
@@ -1108,8 +1143,13 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     int out = 0;
     if ((int)blockIdx.x < g.nhitems) {
         const HItem it = g.hitems[blockIdx.x];
-        if (F.hub[it.hid]) {
-            hub_chunk(g, F, N, it, P, PN, eps, pd, out, c);
+        const int fl = F.hub[it.hid];
+        const long long px = P[ni(it.node)];
+        const long long E = atom_load(&g.excess[it.node]);
+        ctl_words();
+        KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(px), "v"(E));
+        if (c_done && c_act && fl) {
+            hub_chunk(g, F, N, it, px, E, P, PN, eps, pd, out, c);
 #ifdef KS_STAMPS
             kind = 1;
 #endif
@@ -1119,8 +1159,17 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         const int i = ((int)blockIdx.x - g.nhitems - g.sw_clsb) * WPB + (int)(threadIdx.x >> 6);
         if (i < g.ncls_c) {
             const int x = g.obeg[CCLS] + i;
-            if (F.flag[x]) {
-                node_discharge<KS_NB>(g, F, N, x, P, PN, eps, pd, out, c);
+            // flag, excess and record (price, segment) issued together
+            const int fl = F.flag[x];
+            const long long e = atom_load(&g.excess[x]);
+            const long long px = P[ni(x)];
+            const long long sw = g.p0[ni(x) + ND_SEG];
+            ctl_words();
+            KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(e), "v"(px), "v"(sw));
+            const int b0 = (int)(unsigned)((unsigned long long)sw & 0xffffffffULL);
+            const int en = (int)(unsigned)((unsigned long long)sw >> 32);
+            if (c_done && c_act && fl) {
+                node_discharge<KS_NB>(g, F, N, x, e, px, b0, en, PN, P, eps, pd, out, c);
 #ifdef KS_STAMPS
                 kind = 2;
 #endif
@@ -1130,12 +1179,20 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         // class windows, WPW per wave strided across the class blocks
         const int tw = g.sw_clsb * WPB;
         const int w0 = wave_index_in_grid(g.nhitems);
-        unsigned long long mk[WPW];
+        WinFlag wf[WPW];
+        int any_raw = 0;
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
             const int w = w0 + j * tw;
-            mk[j] = w < g.wbeg[CCLS] ? window_mask(g, F.flag, w, true) : 0;
+            wf[j] = w < g.wbeg[CCLS] ? window_load(g, F.flag, w) : WinFlag{-1, 0};
+            any_raw |= wf[j].raw;
         }
+        ctl_words();
+        KS_AFTER_LOADS(c_done, c_act, "v"(any_raw));
+        const bool go = c_done && c_act;
+        unsigned long long mk[WPW];
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) mk[j] = window_take(g, F.flag, w0 + j * tw, wf[j], go);
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
             if (!mk[j]) continue;
@@ -1349,30 +1406,41 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.bf[(seq + 2) % 3].hub[h] = 0;
         if (threadIdx.x == 0) g.ctl->bfa[(seq + 2) % 3] = 0;
     }
-    if (g.ctl->bf_done) return;
-    if (!dense && !g.ctl->bfa[seq % 3]) {   // empty frontier: the update converged
-        if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->bf_done = 1;
-        return;
-    }
     const Front F = g.bf[seq % 3], N = g.bf[(seq + 1) % 3];
     if (threadIdx.x < HUB_LDS) hub_min[threadIdx.x] = INF64;
-    __syncthreads();
+    __syncthreads();   // (waits for outstanding loads: the control words are read after it)
+    // The update is still running (!done) and this round's frontier is non-empty
+    // (dense || any): read in each branch after its first loads and tested only
+    // once they were issued (KS_AFTER_LOADS).
+    int done = 0, any = 0;
+    auto ctl_words = [&]() {
+        done = g.ctl->bf_done;
+        any = g.ctl->bfa[seq % 3];
+    };
 #ifdef KS_STAMPS
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-    int kind = (int)blockIdx.x < g.nhitems ? 1 : 0;
+    int kind = (int)blockIdx.x < g.nhitems * HSPLIT ? 1 : 0;
 #endif
     const long long eps = g.ctl->eps;
     int out = 0;
     long long scans = 0;
-    if ((int)blockIdx.x < g.nhitems) {
-        const HItem it = g.hitems[blockIdx.x];
-        if (dense || F.hub[it.hid]) {
-            const long long dv = atom_load(&g.dist[ni(it.node)]);
+    // Hub chunks are split over HSPLIT workgroups: a relaxation is a dependent
+    // chain (arc, tail record, leaf expansion, atomic), and a thread that runs
+    // several of them in a row made the hub the last block of its round.
+    const int nhb = g.nhitems * HSPLIT;
+    if ((int)blockIdx.x < nhb) {
+        const HItem it = g.hitems[blockIdx.x / HSPLIT];
+        const int sub = (int)blockIdx.x % HSPLIT;
+        const int fl = F.hub[it.hid];
+        const long long dv = atom_load(&g.dist[ni(it.node)]);
+        const long long pv = g.p0[ni(it.node)];
+        ctl_words();
+        KS_AFTER_LOADS(done, any, "v"(fl), "v"(dv), "v"(pv));
+        if (!done && (dense || any) && (dense || fl)) {
             if (PR || dv < INF64) {
-                const long long pv = g.p0[ni(it.node)];
 #pragma unroll
-                for (int k = 0; k < PER_T; ++k) {
-                    const int a = it.begin + threadIdx.x * PER_T + k;
+                for (int k = 0; k < BF_PER_T; ++k) {
+                    const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
                         relax_in<PR>(g, N, a, dv, pv, eps, hub_min, out);
                         scans++;
@@ -1381,8 +1449,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             }
         }
     } else if (dense) {
-        const int w = wave_index_in_grid(g.nhitems);
-        if (w < g.wbeg[CCLS]) {
+        const int w = wave_index_in_grid(nhb);
+        ctl_words();
+        if (done) {
+            // the update already converged
+        } else if (w < g.wbeg[CCLS]) {
             const Scan sc{F.flag, 1};
 #define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, hub_min, out, scans)
             KS_BY_CLASS(w, sc, KS_BF_CALL)
@@ -1391,16 +1462,26 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
         }
     } else {
-        const int tw = ((int)gridDim.x - g.nhitems) * WPB;
-        const int w0 = wave_index_in_grid(g.nhitems);
+        const int tw = ((int)gridDim.x - nhb) * WPB;
+        const int w0 = wave_index_in_grid(nhb);
+        WinFlag wf[WPW];
+        int any_raw = 0;
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            wf[j] = window_load(g, F.flag, w0 + j * tw);
+            any_raw |= wf[j].raw;
+        }
+        ctl_words();
+        KS_AFTER_LOADS(done, any, "v"(any_raw));
+        const bool go = !done && any;
         unsigned long long mk[WPW];
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
             const int w = w0 + j * tw;
-            mk[j] = window_mask(g, F.flag, w, true);
+            mk[j] = window_take(g, F.flag, w, wf[j], go);
             // chunk items: a node's flag is read by all its chunks; the lead chunk
             // clears it two rounds later (in the buffer read by the previous round)
-            if (w >= g.wbeg[CCLS] && w - g.wbeg[CCLS] < g.ncitems && lane_id() == 0) {
+            if (go && w >= g.wbeg[CCLS] && w - g.wbeg[CCLS] < g.ncitems && lane_id() == 0) {
                 const CItem ci = g.citems[w - g.wbeg[CCLS]];
                 if (ci.lead) g.bf[(seq + 2) % 3].flag[ci.node] = 0;
             }
@@ -1440,9 +1521,13 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         }
     }
     if (__any(out) && lane_id() == 0) g.ctl->bfa[(seq + 1) % 3] = 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        atomicAdd(g.ctr + C_BFROUND, 1ULL);
-        g.ctl->bf_count += 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // block 0 is a hub block or a window block: done/any are final here
+        if (!done && (dense || any)) {
+            atomicAdd(g.ctr + C_BFROUND, 1ULL);
+            g.ctl->bf_count += 1;
+        } else if (!done) {
+            g.ctl->bf_done = 1;   // empty frontier: the update converged
+        }
     }
     scans = wave_sum(scans);
 #ifdef KS_STAMPS
@@ -2156,11 +2241,14 @@ struct EngineImpl {
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
-    int dense_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
+    // Bellman-Ford rounds: HSPLIT workgroups per hub chunk, then the windows / chunk items
+    int dense_grid() const { return nhitems * HSPLIT + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
     int sweep_cls_blocks() const { return std::max(1, (wbeg[CCLS] + WPW * WPB - 1) / (WPW * WPB)); }
     // sweeps: hub chunks, class-window blocks, one wave per chunked-class node
     int sweep_grid() const { return nhitems + sweep_cls_blocks() + (ncls[CCLS] + WPB - 1) / WPB; }
-    int sparse_grid() const { return nhitems + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB)); }
+    int sparse_grid() const {
+        return nhitems * HSPLIT + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB));
+    }
     int hi() const { return h_sctl->hi; }
 };
 
@@ -3171,7 +3259,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
             hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
             for (int r = 0; r < kb; ++r) {   // the first round may be the update's dense one
-                hipLaunchKernelGGL(k_bf_round<false>, dim3(r == 0 ? dgrid : sgrid), dim3(BLK), 0, st, g, bseq, -1);
+                // only a cycle's first round can be an update's first (dense) one
+                hipLaunchKernelGGL(k_bf_round<false>, dim3(r == 0 ? dgrid : sgrid), dim3(BLK), 0, st, g, bseq,
+                                   r == 0 ? -1 : 0);
                 ++bseq;
                 ++bf_launches;
             }
@@ -3214,8 +3304,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 continue;
             }
             if (cycle_log)
-                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d\n", phases, eps,
-                             hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1]);
+                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d n_exc %d\n", phases,
+                             eps, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc);
             kb = std::max(8, std::min(256, hc->bf_count - hc->bf_r0 + 6));
             ++gus;
             sweeps += gi;

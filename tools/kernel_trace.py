@@ -38,6 +38,25 @@ def main():
         q = np.percentile(x, [10, 50, 90, 99])
         print(f"{k[:40]:40s} n={len(x):6d} sum={x.sum() / 1e3:8.2f}ms p10={q[0]:6.1f} p50={q[1]:6.1f} "
               f"p90={q[2]:6.1f} p99={q[3]:6.1f} us; <2us: {(x < 2).sum()}")
+    for k in ("k_bf_round<false>", "k_sweep"):
+        x = dur[names == k]
+        if not len(x):
+            continue
+        print(f"{k}: device time by launch duration")
+        edges = [0, 3, 6, 10, 15, 25, 40, 70, 120, 1e9]
+        for lo, hi in zip(edges[:-1], edges[1:]):
+            m = (x >= lo) & (x < hi)
+            if m.any():
+                print(f"   [{lo:4.0f}, {hi:4.0f}) us: n={m.sum():6d} sum={x[m].sum() / 1e3:7.2f} ms")
+    if "--seq" in sys.argv:   # the Bellman-Ford round durations of each update, in launch order
+        cur = []
+        for k, d in zip(names, dur):
+            if k == "k_gu_init":
+                if cur:
+                    print("update:", " ".join(f"{v:.0f}" for v in cur))
+                cur = []
+            elif k == "k_bf_round<false>" and d >= 3:
+                cur.append(d)
     print(f"gaps: n={len(gaps)} sum={gaps.sum() / 1e3:.2f} ms p50={np.median(gaps):.2f} p90={np.percentile(gaps, 90):.2f} us")
 
 
