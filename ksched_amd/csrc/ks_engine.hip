@@ -92,7 +92,13 @@ constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
 
-enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5 };
+enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7 };
+#ifndef KS_AUG_K
+#define KS_AUG_K 64                 // a phase's tail: at most this many excess nodes are augmented directly
+#endif
+constexpr int AUG_K = KS_AUG_K;
+constexpr int AUG_K2 = 256;        // walkers from the nodes a hub distribution fed
+constexpr int AUG_STEPS = 512;     // hops per walk before its units are left where it stands
 
 struct Ctl {
     long long eps;
@@ -108,6 +114,11 @@ struct Ctl {
     int n_exc;             // nodes the last apply found holding excess
     int bf_r0;             // bf_count when the running update started
     int bf_seq0;           // sequence number of the running update's first (dense) round
+    int aug_reached;       // walks of this cycle that reached a deficit / stopped short
+    int aug_short;
+    int n_xl2;             // nodes fed by this cycle's hub distribution
+    int dbg_x[4];          // diagnostics (KS_CYCLE_LOG): the first listed excess nodes, their excess at the apply
+    int dbg_e[4];
 };
 
 struct HItem {
@@ -161,6 +172,9 @@ struct DG {
     int ncls_c;            // nodes of the chunked class
     int sw_clsb;           // sweep blocks striding the class windows (after the hub blocks)
     const int* hnchunks;
+    int* xl;               // excess nodes listed by the last apply (the first AUG_K)
+    int* xl2;              // nodes fed by k_aug_hub (the first AUG_K2)
+    long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
     long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
     long long* q_taken;
     long long* q_min;
@@ -1558,22 +1572,35 @@ __device__ __forceinline__ void clear_fronts(const DG& g, const Front* fs) {
 // GU init: drain hub inboxes, dist = 0 at deficits / INF elsewhere, clean flags.
 // A cycle whose predecessor left its update unconverged (gu_pending) continues
 // that update instead; seq0 = the sequence number of this cycle's first round.
+// The deficits are the first round's frontier (a sparse round: the dense pass
+// over every node cost 16–60 µs per update). Each flag is set by the thread that
+// cleared it (same grid-stride mapping as clear_fronts; hubs: block 0).
 __global__ void k_gu_init(DG g, int seq0) {
     if (g.ctl->gu_pending) return;
     clear_fronts(g, g.bf);
+    const Front F0 = g.bf[seq0 % 3];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
         g.ctl->gu_L = 0;
         g.ctl->bf_r0 = g.ctl->bf_count;
         g.ctl->bf_seq0 = seq0;
         g.ctl->n_exc = 0;
-        for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
+        g.ctl->aug_reached = 0;
+        g.ctl->aug_short = 0;
+        for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = k == seq0 % 3 ? 1 : 0;
     }
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        if (v >= g.hub_base) drain_inbox(g, (int)v - g.hub_base);
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.hub_base; v += (long long)gridDim.x * BLK) {
         const long long e = atom_load(&g.excess[v]);
         g.dist[ni(v)] = e < 0 ? 0 : INF64;
+        if (e < 0) F0.flag[v] = 1;
     }
+    if (blockIdx.x == 0)
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) {
+            drain_inbox(g, h);
+            const long long e = atom_load(&g.excess[g.hub_base + h]);
+            g.dist[ni(g.hub_base + h)] = e < 0 ? 0 : INF64;
+            if (e < 0) F0.hub[h] = 1;
+        }
 }
 
 // PR init: dist = 0 everywhere.
@@ -1609,7 +1636,11 @@ __global__ void k_gu_max(DG g) {
     clear_fronts(g, g.sf);
     if (blockIdx.x == 0) {
         for (int k = threadIdx.x; k < MAXB; k += BLK) g.ctl->sweep_act[k] = 0;
-        if (threadIdx.x == 0) g.ctl->apply_act = 0;
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.aug_req[h] = 0;
+        if (threadIdx.x == 0) {
+            g.ctl->apply_act = 0;
+            g.ctl->n_xl2 = 0;
+        }
     }
     if (!g.ctl->bf_done) return;
     long long mx = 0;
@@ -1636,7 +1667,7 @@ __global__ void k_gu_apply(DG g, int sseq) {
     long long L = g.ctl->gu_L;
     L = L < lim ? L : lim;
     const Front F = g.sf[sseq % 3];
-    int out = 0;
+    int out = 0, xv = -1;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = atom_load(&g.dist[ni(v)]);
         const long long e = atom_load(&g.excess[v]);
@@ -1645,12 +1676,227 @@ __global__ void k_gu_apply(DG g, int sseq) {
         const long long np = g.p0[ni(v)] - eps * dd;
         g.p0[ni(v)] = np;
         g.p1[ni(v)] = np;
-        if (e > 0) mark(g, F, (int)v, out);
+        if (e > 0) {
+            mark(g, F, (int)v, out);
+            xv = (int)v;
+        }
     }
+    // count the excess nodes (one atomic per wave) and list the first AUG_K for k_augment
     const unsigned long long ex = __ballot(out);
+    int base = 0;
     if (ex && lane_id() == 0) {
         g.ctl->apply_act = 1;
-        atomicAdd(&g.ctl->n_exc, (int)__popcll(ex));
+        base = atomicAdd(&g.ctl->n_exc, (int)__popcll(ex));
+    }
+    base = __shfl(base, 0);
+    if (out) {
+        const int idx = base + (int)__popcll(ex & ((1ULL << lane_id()) - 1));
+        if (idx < AUG_K) g.xl[idx] = xv;
+        if (idx < 4) {
+            g.ctl->dbg_x[idx] = xv;
+            g.ctl->dbg_e[idx] = (int)atom_load(&g.excess[xv]);
+        }
+    }
+}
+
+// Hub distribution (between the two walker passes): a hub that holds excess
+// (the cluster aggregator collects the units the walkers bring it) hands it to
+// its admissible arcs towards no larger distance, one workgroup per
+// 1024-arc chunk claiming its share with one returning atomic (as the sweeps'
+// hub chunks do); the fed nodes are listed for the second walker pass.
+__global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq) {
+    __shared__ long long sh[WPB];
+    __shared__ long long s_take;
+    if (!g.ctl->bf_done) return;
+    const int nx = g.ctl->n_exc;
+    if (nx == 0 || nx > AUG_K) return;
+    const HItem it = g.hitems[blockIdx.x];
+    const int x = it.node;
+    const long long E = atom_load(&g.excess[x]);
+    if (E <= 0) return;
+    const Front F = g.sf[sseq % 3];
+    const long long eps = g.ctl->eps;
+    const long long dx = atom_load(&g.dist[ni(x)]);
+    const long long px = g.p0[ni(x)];
+    long long r[PER_T], adm[PER_T], uc[PER_T];
+    int w[PER_T], rv[PER_T];
+    long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        r[k] = 0;
+        w[k] = 0;
+        rv[k] = 0;
+        uc[k] = 0;
+        adm[k] = 0;
+        if (a < it.end) {
+            r[k] = atom_load(&g.rcap[a]);   // the first walker pass claimed with atomics
+            w[k] = g.head[a];
+            rv[k] = g.rev[a];
+            uc[k] = g.ucap[a];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        if (a < it.end && r[k] > 0) {
+            const long long cr = g.cost[a] + px - g.p0[ni(w[k])];
+            const long long dw = atom_load(&g.dist[ni(w[k])]);
+            if (cr <= eps && (dw < dx || (dw == dx && cr < 0))) adm[k] = r[k];
+        }
+        mine += adm[k];
+    }
+    long long Ac = 0;
+    const long long excl = block_excl_scan(mine, sh, &Ac);
+    if (threadIdx.x == 0) {
+        long long take = 0;
+        if (Ac > 0) {
+            const long long start = atom_add_ret(&g.aug_req[it.hid], Ac);
+            take = E - start;
+            take = take < 0 ? 0 : (take > Ac ? Ac : take);
+        }
+        s_take = take;
+        if (take) atom_add(&g.excess[x], -take);
+    }
+    __syncthreads();
+    long long rt = s_take - excl;
+    rt = rt < 0 ? 0 : (rt > mine ? mine : rt);
+    int dummy = 0;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const long long d = adm[k] < rt ? adm[k] : rt;
+        rt -= d;
+        if (d <= 0) continue;
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        g.rcap[a] = r[k] - d;              // only this chunk touches the pair in this kernel
+        g.rcap[rv[k]] = uc[k] - (r[k] - d);
+        const long long now = atom_add_ret(&g.excess[w[k]], d) + d;
+        if (now > 0) {
+            mark(g, F, w[k], dummy);
+            const int idx = atomicAdd(&g.ctl->n_xl2, 1);
+            if (idx < AUG_K2) g.xl2[idx] = w[k];
+        }
+    }
+}
+
+// ------------------------------------------------------- tail augmentation ---
+// When a converged update leaves at most AUG_K nodes with excess (the tail of a
+// phase: a few units that the sweeps would move one hop per sweep over dozens
+// of update cycles — measured: ~100 cycles for the last ~50 units of a config-4
+// round), each of them sends its excess straight down the update's distances:
+// one wave per excess node walks from u along the residual arc (u, w) of least
+// distance d(w), until it reaches a deficit. An arc qualifies if d(w) < d(u)
+// (or d(w) = d(u) and it is admissible) and its reduced cost under the updated
+// prices is at most ε: the reverse arc a push creates then has reduced cost
+// ≥ −ε, so ε-optimality holds (the update's tree arcs have rc ∈ [−ε, 0); arcs
+// one length unit off the tree, rc ∈ [0, ε), let several units leave a node
+// whose tree arc carries one). Walkers claim residual capacity with a CAS
+// (they may share arcs); units that cannot go on (no arc, capacity taken, a
+// hub, the hop limit) stay where the walk stands, marked for the sweeps that
+// follow. Runs between the apply and the cycle's sweeps.
+// mode 0: from the apply's excess nodes (non-hubs); mode 1: from the nodes a hub
+// distribution (k_aug_hub) fed.
+__global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode) {
+    if (!g.ctl->bf_done) return;
+    const int nx = g.ctl->n_exc;
+    if (nx == 0 || nx > AUG_K) return;
+    const int cnt = mode ? min(g.ctl->n_xl2, AUG_K2) : nx;
+    if ((int)blockIdx.x >= cnt) return;
+    const int lane = lane_id();
+    const Front F = g.sf[sseq % 3];
+    const long long eps = g.ctl->eps;
+    int u = mode ? g.xl2[blockIdx.x] : g.xl[blockIdx.x];
+    if (u < 0 || u >= g.hub_base) return;   // hubs: k_aug_hub
+    long long carry = 0;
+    if (lane == 0) carry = atom_exch(&g.excess[u], 0LL);
+    carry = __shfl(carry, 0);
+    if (carry <= 0) {
+        if (lane == 0 && carry < 0) atom_add(&g.excess[u], carry);   // (not an excess node any more)
+        return;
+    }
+    long long du = atom_load(&g.dist[ni(u)]);
+    long long pu = g.p0[ni(u)];
+    int hops = 0, reached = 0, dummy = 0;
+    for (int step = 0; step < AUG_STEPS; ++step) {
+        int b0, en;
+        seg_of(g.p0, u, b0, en);
+        // the admissible residual arc of least d(w) ≤ d(u) (ties: lowest position)
+        long long bd = INF64;
+        int ba = -1;
+        for (int base = b0; base < en; base += WAVE) {
+            const int a = base + lane;
+            long long key = INF64;
+            if (a < en) {
+                const long long r = atom_load(&g.rcap[a]);   // other walkers claim with atomics
+                const int w = g.head[a];
+                const long long cr = g.cost[a] + pu - g.p0[ni(w)];
+                const long long dw = atom_load(&g.dist[ni(w)]);
+                if (r > 0 && cr <= eps && (dw < du || (dw == du && cr < 0))) key = dw;
+            }
+            const long long mn = wave_min(key);
+            if (mn < bd) {
+                const unsigned long long hit = __ballot(key == mn);
+                bd = mn;
+                ba = base + __ffsll((long long)hit) - 1;
+            }
+        }
+        if (ba < 0) break;
+        // claim min(carry, residual) on arc ba
+        long long take = 0;
+        int w = 0;
+        if (lane == 0) {
+            w = g.head[ba];
+            long long r = atom_load(&g.rcap[ba]);
+            for (;;) {
+                take = r < carry ? r : carry;
+                if (take <= 0) {
+                    take = 0;
+                    break;
+                }
+                long long exp = r;
+                if (__hip_atomic_compare_exchange_strong(&g.rcap[ba], &exp, r - take, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    break;
+                r = exp;
+            }
+            if (take > 0) atom_add(&g.rcap[g.rev[ba]], take);
+            if (take < carry) {   // the rest stays at u
+                atom_add(&g.excess[u], carry - take);
+                mark(g, F, u, dummy);
+            }
+        }
+        take = __shfl(take, 0);
+        w = __shfl(w, 0);
+        if (take == 0) {
+            carry = 0;   // deposited at u above
+            break;
+        }
+        carry = take;
+        ++hops;
+        u = w;
+        du = bd;
+        if (lane == 0) {
+            const long long e = atom_load(&g.excess[u]);
+            if (e < 0 || u >= g.hub_base) {   // a deficit (or a hub: the sweeps take over)
+                const long long now = atom_add_ret(&g.excess[u], carry) + carry;
+                if (now > 0) mark(g, F, u, dummy);
+                reached = e < 0 ? 1 : 0;
+                carry = 0;
+            }
+        }
+        carry = __shfl(carry, 0);
+        if (carry == 0) break;
+        pu = g.p0[ni(u)];
+    }
+    if (lane == 0) {
+        if (carry > 0) {   // hop limit or no admissible arc: the units stay at u
+            atom_add(&g.excess[u], carry);
+            mark(g, F, u, dummy);
+        }
+        const int sh = (int)blockIdx.x & (CTR_SHARDS - 1);
+        atomicAdd(reached ? &g.ctl->aug_reached : &g.ctl->aug_short, 1);
+        if (reached) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, 1ULL);
+        if (hops) atomicAdd(g.ctr + sh * NCTR + C_AUGHOP, (unsigned long long)hops);
     }
 }
 
@@ -2063,6 +2309,8 @@ struct EngineImpl {
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
+    DBuf<int> xl, xl2;                 // walker start nodes (k_augment)
+    DBuf<long long> aug_req;           // per hub claim counter (k_aug_hub)
     DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;        // pinned host mirror
@@ -2131,7 +2379,7 @@ struct EngineImpl {
         for (auto& b : cls_list) b.release();
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
         q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
-        flags.release(); hubflags.release(); ctr.release(); ctl.release(); saved_flows.release(); p_slot.release();
+        flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
@@ -2223,6 +2471,9 @@ struct EngineImpl {
         g.sw_clsb = sweep_cls_blocks();
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
+        g.xl = xl.p;
+        g.xl2 = xl2.p;
+        g.aug_req = aug_req.p;
         g.q_req = q_req.p;
         g.q_taken = q_taken.p;
         g.q_min = q_min.p;
@@ -2290,6 +2541,8 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     }
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
+    KS_CHECK(s.xl.ensure(AUG_K));
+    KS_CHECK(s.xl2.ensure(AUG_K2));
     KS_CHECK(s.sctl.ensure(1));
     KS_CHECK(hipMemset(s.sctl.p, 0, sizeof(StoreCtl)));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
@@ -2657,6 +2910,7 @@ static int build(EngineImpl& s, std::string& err) {
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
         const int nq = std::max(1, s.nheavy);
         KS_CHECK(s.q_req.ensure(nq));
+        KS_CHECK(s.aug_req.ensure(nq));
         KS_CHECK(s.q_taken.ensure(nq));
         KS_CHECK(s.q_min.ensure(nq));
         KS_CHECK(s.q_unsat.ensure(nq));
@@ -3157,7 +3411,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
-    const bool cycle_log = std::getenv("KS_CYCLE_LOG") != nullptr;   // diagnostic: one stderr line per cycle
+    const bool cycle_log = std::getenv("KS_CYCLE_LOG") != nullptr;
+    const int nhit = s.nhitems;
+    bool use_aug = true;   // tail augmentation (KS_AUG=0 disables it)
+    if (const char* ea = std::getenv("KS_AUG")) use_aug = std::atoi(ea) != 0;
+    int gi_tail = 4;       // sweeps per cycle once at most AUG_K nodes hold excess (even)
+    if (const char* et = std::getenv("KS_TAIL_GI")) gi_tail = std::max(2, std::min(MAXB, std::atoi(et))) & ~1;   // diagnostic: one stderr line per cycle
     // A phase that another phase follows may end with a few excess nodes left:
     // refine's start (saturate every negative reduced cost) accepts any
     // pseudoflow, so the next, finer phase absorbs them with its own excess.
@@ -3252,16 +3511,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 && use_warm ? warm_thr : 0LL);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         uint64_t phase_sweeps = 0;
-        const int gi = gi_base;
+        int gi = gi_base;     // sweeps in the next cycle (fewer in a phase's tail, where walks augment)
         int phase_peak = 0;   // most excess nodes seen by an update of this phase
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][gi sweeps][end: control block → pinned host memory].
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
             hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
             for (int r = 0; r < kb; ++r) {   // the first round may be the update's dense one
-                // only a cycle's first round can be an update's first (dense) one
-                hipLaunchKernelGGL(k_bf_round<false>, dim3(r == 0 ? dgrid : sgrid), dim3(BLK), 0, st, g, bseq,
-                                   r == 0 ? -1 : 0);
+                // sparse from the first round: k_gu_init flags the deficits
+                hipLaunchKernelGGL(k_bf_round<false>, dim3(sgrid), dim3(BLK), 0, st, g, bseq, 0);
                 ++bseq;
                 ++bf_launches;
             }
@@ -3270,6 +3528,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
+            if (use_aug) {   // tail augmentation: walkers, hub distribution, walkers from what it fed
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0);
+                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1);
+            }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
             sseq += gi;
@@ -3303,9 +3566,18 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 cur ^= 1;
                 continue;
             }
-            if (cycle_log)
-                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d n_exc %d\n", phases,
-                             eps, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc);
+            if (cycle_log) {
+                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d n_exc %d walks %d/%d",
+                             phases, eps, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc,
+                             hc->aug_reached, hc->aug_short);
+                for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
+                    const int x = hc->dbg_x[k];
+                    int c = 0;
+                    while (c < NGC && x >= s.obeg[c + 1]) ++c;
+                    std::fprintf(stderr, " [x%d c%d e%d]", x, x >= s.hub_base ? 9 : c, hc->dbg_e[k]);
+                }
+                std::fprintf(stderr, "\n");
+            }
             kb = std::max(8, std::min(256, hc->bf_count - hc->bf_r0 + 6));
             ++gus;
             sweeps += gi;
@@ -3324,6 +3596,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
+            gi = (use_aug && hc->n_exc <= AUG_K) ? gi_tail : gi_base;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
@@ -3393,6 +3666,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     unsigned long long tc[NCTR] = {0};
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
+    if (cycle_log)
+        std::fprintf(stderr, "solve tail walks to a deficit %llu, hops %llu\n", tc[C_AUGWALK], tc[C_AUGHOP]);
 
 #ifdef KS_STAMPS
     if (stamp_path && s.stamps.n > 1) {
