@@ -1704,7 +1704,7 @@ __global__ void k_gu_apply(DG g, int sseq) {
 // its admissible arcs towards no larger distance, one workgroup per
 // 1024-arc chunk claiming its share with one returning atomic (as the sweeps'
 // hub chunks do); the fed nodes are listed for the second walker pass.
-__global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq) {
+__global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
     if (!g.ctl->bf_done) return;
@@ -1742,7 +1742,7 @@ __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq) {
         if (a < it.end && r[k] > 0) {
             const long long cr = g.cost[a] + px - g.p0[ni(w[k])];
             const long long dw = atom_load(&g.dist[ni(w[k])]);
-            if (cr <= eps && (dw < dx || (dw == dx && cr < 0))) adm[k] = r[k];
+            if (cr <= slack * eps && (dw < dx || (dw == dx && cr < 0))) adm[k] = r[k];
         }
         mine += adm[k];
     }
@@ -1796,7 +1796,7 @@ __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq) {
 // follow. Runs between the apply and the cycle's sweeps.
 // mode 0: from the apply's excess nodes (non-hubs); mode 1: from the nodes a hub
 // distribution (k_aug_hub) fed.
-__global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode) {
+__global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int slack) {
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
     if (nx == 0 || nx > AUG_K) return;
@@ -1831,7 +1831,7 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode) {
                 const int w = g.head[a];
                 const long long cr = g.cost[a] + pu - g.p0[ni(w)];
                 const long long dw = atom_load(&g.dist[ni(w)]);
-                if (r > 0 && cr <= eps && (dw < du || (dw == du && cr < 0))) key = dw;
+                if (r > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
             }
             const long long mn = wave_min(key);
             if (mn < bd) {
@@ -3415,6 +3415,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int nhit = s.nhitems;
     bool use_aug = true;   // tail augmentation (KS_AUG=0 disables it)
     if (const char* ea = std::getenv("KS_AUG")) use_aug = std::atoi(ea) != 0;
+    int aug_slack = 4;     // walks take arcs of reduced cost <= aug_slack·ε (KS_AUG_SLACK)
+    if (const char* es = std::getenv("KS_AUG_SLACK")) aug_slack = std::max(1, std::atoi(es));
     int gi_tail = 4;       // sweeps per cycle once at most AUG_K nodes hold excess (even)
     if (const char* et = std::getenv("KS_TAIL_GI")) gi_tail = std::max(2, std::min(MAXB, std::atoi(et))) & ~1;   // diagnostic: one stderr line per cycle
     // A phase that another phase follows may end with a few excess nodes left:
@@ -3529,9 +3531,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             if (use_aug) {   // tail augmentation: walkers, hub distribution, walkers from what it fed
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0);
-                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq);
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, aug_slack);
+                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, aug_slack);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, aug_slack);
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
