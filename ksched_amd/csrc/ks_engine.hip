@@ -3531,9 +3531,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             if (use_aug) {   // tail augmentation: walkers, hub distribution, walkers from what it fed
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, aug_slack);
-                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, aug_slack);
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, aug_slack);
+                // slack > 1 only while a finer phase or price refinement still follows (ε > 1):
+                // a phase at ε = 1 must end 1-optimal
+                const int sl = eps > 1 ? aug_slack : 1;
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, sl);
+                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, sl);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, sl);
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);

@@ -19,7 +19,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run 
     || { echo "rocprof failed"; tail -30 "$OUT/bench_prof.err"; exit 1; }
 python tools/prof_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv" && head -6 "$OUT/kernel_stats.csv"
 tools/gpu_pmc.sh "$TAG/pmc" || exit 1
-tools/gpu_calib.sh "$TAG/calib" || exit 1
+# FETCH_SIZE calibration (tools/gpu_calib.sh) is a one-off: profiles/r02_fetch_calibration.json
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 2 > "$OUT/bench.json" 2> "$OUT/bench.err" \
     || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
 python -c "import json; d=json.load(open('$OUT/bench.json')); print('full', d['ms_per_step'], d['value'], d['cpu_baseline']['value'], d['parity']['match'])"

@@ -3,7 +3,7 @@
 calibration run (gpu_calib.sh): per kernel, raw FETCH_SIZE + WRITE_SIZE bytes
 per launch, the calibrated range, and atomic request counts / rates.
 
-    python tools/pmc_traffic.py gpurun_out/<pmc tag> gpurun_out/<calib tag> DATE > profiles/r02_pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/<pmc tag> gpurun_out/<calib tag>|<profile.json> DATE > profiles/<tag>_pmc_traffic.json
 """
 import csv
 import json
@@ -29,15 +29,18 @@ def per_kernel(dirs):
 def main():
     pmc, cal, date = sys.argv[1], sys.argv[2], sys.argv[3]
     k = per_kernel([os.path.join(pmc, p) for p in ("fetch", "write", "atom", "ta")])
-    c = per_kernel([os.path.join(cal, "pmc_FETCH_SIZE"), os.path.join(cal, "pmc_WRITE_SIZE")])
-    known = json.load(open(os.path.join(cal, "calib_FETCH_SIZE.json")))
-    calib = {
-        "stream8_fetch_per_byte": c["k_stream8"]["FETCH_SIZE"] * 1024 / known["k_stream8"],
-        "stream4_fetch_per_byte": c["k_stream4"]["FETCH_SIZE"] * 1024 / known["k_stream4"],
-        "gather8_fetch_bytes_per_load": c["k_gather8"]["FETCH_SIZE"] * 1024 / known["k_gather8_loads"],
-        "store8_write_per_byte": c["k_store8"]["WRITE_SIZE"] * 1024 / known["k_store8"],
-        "atomic8_write_bytes_per_op": c["k_atomic8"]["WRITE_SIZE"] * 1024 / known["k_atomic8_ops"],
-    }
+    if cal.endswith(".json"):   # a committed profile's calibration (the calibration is a one-off)
+        calib = json.load(open(cal))["calibration"]
+    else:
+        c = per_kernel([os.path.join(cal, "pmc_FETCH_SIZE"), os.path.join(cal, "pmc_WRITE_SIZE")])
+        known = json.load(open(os.path.join(cal, "calib_FETCH_SIZE.json")))
+        calib = {
+            "stream8_fetch_per_byte": c["k_stream8"]["FETCH_SIZE"] * 1024 / known["k_stream8"],
+            "stream4_fetch_per_byte": c["k_stream4"]["FETCH_SIZE"] * 1024 / known["k_stream4"],
+            "gather8_fetch_bytes_per_load": c["k_gather8"]["FETCH_SIZE"] * 1024 / known["k_gather8_loads"],
+            "store8_write_per_byte": c["k_store8"]["WRITE_SIZE"] * 1024 / known["k_store8"],
+            "atomic8_write_bytes_per_op": c["k_atomic8"]["WRITE_SIZE"] * 1024 / known["k_atomic8_ops"],
+        }
     times = {}
     stats = os.path.join(pmc, "kernel_stats.csv")
     if os.path.exists(stats):
