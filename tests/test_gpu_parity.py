@@ -274,3 +274,22 @@ def test_mapping_with_flow_cycles_terminates_and_respects_pus(ctx):
         r = ctx.solve()
         assert (r.cost, r.flow) == (cost, fv), trial
         check_mapping(g, ctx.task_mapping())
+
+
+@pytest.mark.parametrize("env", [{"KS_AUG": "0"}, {"KS_AUG_SLACK": "1"}, {"KS_AUG_SLACK": "4", "KS_TAIL_GI": "2"}])
+def test_tail_walks_do_not_change_the_optimum(ctx, monkeypatch, env):
+    """The phase-tail walks (k_augment / k_aug_hub) off, at slack 1
+    (ε-optimality kept) and at the default slack with the fewest tail sweeps: the
+    same optimal cost and flow, the flow re-verified by the oracle — on a
+    config-2-sized Quincy cell (hub excess in every phase's tail) and on random
+    graphs with several deficits, lower bounds and parallel paths."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)      # read by the engine at every ks_solve
+    g = gen.quincy(10_000, 1_000, 25, 100, 2)
+    st, c, fv, _, _ = ko.ssp(g)
+    assert st == 0
+    solve_and_check(ctx, g, c, fv)
+    for trial, g in random_graphs(777, 15):
+        st, c, fv, _, _ = ko.ssp(g)
+        if st == 0:
+            solve_and_check(ctx, g, c, fv)
