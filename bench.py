@@ -77,6 +77,23 @@ def roofline_of(results):
         a44 = B_RELAX * units / (ms / 1e3) / 1e9 if ms > 0 else 0.0
         line["achieved_44B"] = round(a44, 3)
         line["frac_44B"] = round(a44 / HBM_PEAK_GBS, 6)
+    # SURVEY §8(d) solve-level figure: B_work = 24 B × (arc scans + node visits + pushes)
+    # over the whole solve time (and with the Bellman-Ford relaxations added), and the
+    # single-pass floor B_pass = 2m·16 + n·24 for scale
+    t_solve = sum(r.raw["ms"]["total"] for r in results) / 1e3
+    if t_solve > 0:
+        nn, mm = results[-1].raw["n_nodes"], results[-1].raw["n_arcs"]
+        bw = B_UNIT * sw_units
+        bwa = B_UNIT * (sw_units + bf_units)
+        bp = 2 * mm * 16 + nn * 24
+        line["solve_level"] = {
+            "b_work_bytes": bw, "achieved": round(bw / t_solve / 1e9, 3),
+            "frac": round(bw / t_solve / 1e9 / HBM_PEAK_GBS, 6),
+            "b_work_with_bf_bytes": bwa, "achieved_with_bf": round(bwa / t_solve / 1e9, 3),
+            "frac_with_bf": round(bwa / t_solve / 1e9 / HBM_PEAK_GBS, 6),
+            "b_pass_bytes": bp, "b_pass_us_at_peak": round(bp / (HBM_PEAK_GBS * 1e9) * 1e6, 2),
+            "note": "SURVEY 8(d): B_work / t_solve over all timed solves; b_pass = one read of the "
+                    "residual graph, the floor any iterative solve sits above"}
     if os.path.exists(PMC_FILE):
         pmc = json.load(open(PMC_FILE))
         k = pmc.get("kernels", {}).get(kernel, {})

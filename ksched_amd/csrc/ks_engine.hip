@@ -3417,6 +3417,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     if (const char* ea = std::getenv("KS_AUG")) use_aug = std::atoi(ea) != 0;
     int aug_slack = 4;     // walks take arcs of reduced cost <= aug_slack·ε (KS_AUG_SLACK)
     if (const char* es = std::getenv("KS_AUG_SLACK")) aug_slack = std::max(1, std::atoi(es));
+    // Bellman-Ford rounds enqueued per cycle: the last update's count + kb_margin,
+    // at least kb_min (a launch that finds the update converged still costs ≈ 5 µs
+    // with the gap before the next kernel; an update that needs more than was
+    // enqueued costs a whole extra cycle)
+    int kb_margin = 6, kb_min = 8;
+    if (const char* km = std::getenv("KS_KB_MARGIN")) kb_margin = std::max(0, std::atoi(km));
+    if (const char* kn = std::getenv("KS_KB_MIN")) kb_min = std::max(1, std::atoi(kn));
     int gi_tail = 4;       // sweeps per cycle once at most AUG_K nodes hold excess (even)
     if (const char* et = std::getenv("KS_TAIL_GI")) gi_tail = std::max(2, std::min(MAXB, std::atoi(et))) & ~1;   // diagnostic: one stderr line per cycle
     // A phase that another phase follows may end with a few excess nodes left:
@@ -3583,7 +3590,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
                 std::fprintf(stderr, "\n");
             }
-            kb = std::max(8, std::min(256, hc->bf_count - hc->bf_r0 + 6));
+            kb = std::max(kb_min, std::min(256, hc->bf_count - hc->bf_r0 + kb_margin));
             ++gus;
             sweeps += gi;
             sweep_launches += gi;
