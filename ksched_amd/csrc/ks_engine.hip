@@ -82,6 +82,9 @@ constexpr int WPW = KS_WPW;        // windows per wave in sparse (grid-stride) p
 #ifndef KS_NB
 #define KS_NB 4                    // chunked-node discharge: 64-arc batches in flight per wave
 #endif
+#ifndef KS_CHUNK_BLK
+#define KS_CHUNK_BLK 1             // sweeps: one workgroup per chunked-class node (0: one wave)
+#endif
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -1031,6 +1034,90 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
     }
 }
 
+// Whole-node discharge by one workgroup (chunked class; KS_CHUNK_BLK): 512 arcs
+// per pass (two per thread, all loads issued together), the excess distributed
+// by one block-wide scan. A rack (≈ 440 arcs) is one pass — with one wave per
+// node it took two dependent batches, and the chunked node was the last block
+// of almost every sweep (tools/stamps.py).
+__device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, int x, long long e, long long px,
+                                   int b0, int en, long long* __restrict__ PN, const long long* __restrict__ P,
+                                   long long eps, Pend& pd, int& out, Cnt& c) {
+    __shared__ long long sh[WPB];
+    if (threadIdx.x == 0) F.flag[x] = 0;   // the block consumes the node's flag
+    if (e <= 0) return;                    // block-uniform
+    if (threadIdx.x == 0) c.visit++;
+    long long rem = e, minc = INF64;
+    for (int base = b0; base < en; base += 2 * BLK) {   // block-uniform trip count
+        long long r[2], cs[2], pw[2], uc[2], adm[2], cr[2];
+        int w[2], rv[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int a = base + j * BLK + (int)threadIdx.x;
+            r[j] = 0;
+            cs[j] = 0;
+            w[j] = 0;
+            rv[j] = 0;
+            uc[j] = 0;
+            if (a < en) {
+                r[j] = g.rcap[a];
+                w[j] = g.head[a];
+                cs[j] = g.cost[a];
+                rv[j] = g.rev[a];
+                uc[j] = g.ucap[a];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) pw[j] = (base + j * BLK + (int)threadIdx.x < en) ? P[ni(w[j])] : 0;
+        long long mine = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool valid = base + j * BLK + (int)threadIdx.x < en;
+            cr[j] = cs[j] + px - pw[j];
+            adm[j] = (valid && cr[j] < 0 && r[j] > 0) ? r[j] : 0;
+            mine += adm[j];
+        }
+        long long tot = 0;
+        const long long excl = block_excl_scan(mine, sh, &tot);
+        long long avail = rem - excl;   // units this thread's arcs may take, in arc order
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int a = base + j * BLK + (int)threadIdx.x;
+            long long d = avail < adm[j] ? avail : adm[j];
+            d = d < 0 ? 0 : d;
+            avail -= d;
+            if (d > 0) {
+                push_arc(g, &N, a, w[j], r[j], d, pd, out, rv[j], uc[j]);
+                c.push++;
+            }
+            if (a < en) {
+                c.scan++;
+                if (cr[j] < 0) {
+                    if (r[j] - d > 0) minc = min(minc, cr[j]);
+                } else if (r[j] > 0 || cr[j] <= eps) {
+                    minc = min(minc, cr[j]);
+                }
+            }
+        }
+        flush_pending(g, &N, pd, out);
+        rem -= tot < rem ? tot : rem;
+        if (rem == 0) break;   // no relabel needed: the rest of the arcs need no scan
+    }
+    minc = block_min(minc, sh);
+    if (threadIdx.x == 0) {
+        const long long pushed = e - rem;
+        if (pushed) atom_add(&g.excess[x], -pushed);
+        long long np = px;
+        if (rem > 0) {
+            if (minc >= INF64) g.ctl->infeasible = 1;
+            else np = px - (minc + eps);
+            c.relabel++;
+            N.flag[x] = 1;
+            out = 1;
+        }
+        PN[ni(x)] = np;
+    }
+}
+
 // ------------------------------------------------------ grid-stride windows ---
 // Sparse passes use a one-generation grid: each wave owns WPW windows (class
 // windows, then chunk items) strided across the grid, ballots all their flags
@@ -1169,8 +1256,10 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
 #endif
         }
     } else if ((int)blockIdx.x >= g.nhitems + g.sw_clsb) {
-        // chunked class: one wave per node, so no wave serialises two of them
-        const int i = ((int)blockIdx.x - g.nhitems - g.sw_clsb) * WPB + (int)(threadIdx.x >> 6);
+        // chunked class: one workgroup per node (KS_CHUNK_BLK) or one wave per node,
+        // so no wave serialises two of them
+        const int i = KS_CHUNK_BLK ? (int)blockIdx.x - g.nhitems - g.sw_clsb
+                                   : ((int)blockIdx.x - g.nhitems - g.sw_clsb) * WPB + (int)(threadIdx.x >> 6);
         if (i < g.ncls_c) {
             const int x = g.obeg[CCLS] + i;
             // flag, excess and record (price, segment) issued together
@@ -1182,7 +1271,23 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(e), "v"(px), "v"(sw));
             const int b0 = (int)(unsigned)((unsigned long long)sw & 0xffffffffULL);
             const int en = (int)(unsigned)((unsigned long long)sw >> 32);
-            if (c_done && c_act && fl) {
+            if (KS_CHUNK_BLK) {
+                // the flag and the excess may change under the block's feet (pushes into
+                // x, the flag cleared by thread 0): thread 0's reading decides for all
+                __shared__ long long s_e;
+                __shared__ int s_go;
+                if (threadIdx.x == 0) {
+                    s_e = e;
+                    s_go = c_done && c_act && fl;
+                }
+                __syncthreads();
+                if (s_go) {
+                    node_discharge_blk(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
+#ifdef KS_STAMPS
+                    kind = 2;
+#endif
+                }
+            } else if (c_done && c_act && fl) {
                 node_discharge<KS_NB>(g, F, N, x, e, px, b0, en, PN, P, eps, pd, out, c);
 #ifdef KS_STAMPS
                 kind = 2;
@@ -2496,7 +2601,9 @@ struct EngineImpl {
     int dense_grid() const { return nhitems * HSPLIT + std::max(1, (wbeg[CCLS] + ncitems + WPB - 1) / WPB); }
     int sweep_cls_blocks() const { return std::max(1, (wbeg[CCLS] + WPW * WPB - 1) / (WPW * WPB)); }
     // sweeps: hub chunks, class-window blocks, one wave per chunked-class node
-    int sweep_grid() const { return nhitems + sweep_cls_blocks() + (ncls[CCLS] + WPB - 1) / WPB; }
+    int sweep_grid() const {
+        return nhitems + sweep_cls_blocks() + (KS_CHUNK_BLK ? ncls[CCLS] : (ncls[CCLS] + WPB - 1) / WPB);
+    }
     int sparse_grid() const {
         return nhitems * HSPLIT + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB));
     }
