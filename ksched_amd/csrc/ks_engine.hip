@@ -138,7 +138,10 @@ struct CItem {                     // one 64-arc chunk of a chunked-class node
     int node, begin, end, lead;    // lead = 1 for the node's first chunk
 };
 // A wave owns one window: win_batches(c) batches of 64/G consecutive node ids.
-__host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
+#ifndef KS_WB_CUT
+#define KS_WB_CUT 4                // classes below this own two batches per window, the rest one
+#endif
+__host__ __device__ constexpr int win_batches(int c) { return c < KS_WB_CUT ? 2 : 1; }
 static_assert(NGC == 6, "KS_BY_CLASS dispatches six classes");
 __host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
 
