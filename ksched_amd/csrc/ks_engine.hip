@@ -3517,7 +3517,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
     int gi_base = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
-    const int pr_cap = 160;                        // price-refinement rounds before giving up
+    int pr_cap = 160;                              // price-refinement rounds before giving up (KS_PR_CAP)
+    if (const char* pc = std::getenv("KS_PR_CAP")) pr_cap = std::max(1, std::atoi(pc));
     const bool use_pr = s.opts.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
@@ -3534,6 +3535,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     int kb_margin = 6, kb_min = 8;
     if (const char* km = std::getenv("KS_KB_MARGIN")) kb_margin = std::max(0, std::atoi(km));
     if (const char* kn = std::getenv("KS_KB_MIN")) kb_min = std::max(1, std::atoi(kn));
+    bool pr_failed = false;   // the last phase's refinement did not certify the flow
+    bool pr_fail_thr = true;  // KS_PRFAIL_THR=0: the next phase saturates every negative arc
+    if (const char* pf = std::getenv("KS_PRFAIL_THR")) pr_fail_thr = std::atoi(pf) != 0;
     int gi_tail = 4;       // sweeps per cycle once at most AUG_K nodes hold excess (even)
     if (const char* et = std::getenv("KS_TAIL_GI")) gi_tail = std::max(2, std::min(MAXB, std::atoi(et))) & ~1;   // diagnostic: one stderr line per cycle
     // A phase that another phase follows may end with a few excess nodes left:
@@ -3547,7 +3551,24 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     int phase_exit = 256, phase_frac = 128;
     if (const char* pe = std::getenv("KS_PHASE_EXIT")) phase_exit = std::max(0, std::atoi(pe));
     if (const char* pf = std::getenv("KS_PHASE_FRAC")) phase_frac = std::max(1, std::atoi(pf));
+    // ε schedule: the phase that price refinement certifies runs at 1/D of a cost
+    // unit (D = 48; KS_FINAL_DIV), the others at α-multiples of it, the first in
+    // [max|cost|/α², max|cost|/α) scaled. Measured on config 3 (40 solves each):
+    // ending at 1/32 of a unit (the plain max|cost|/α^k sequence) left the flow
+    // short of optimal in 15 of 40 solves — a sixth phase, ≈ 28 ms — at 1/48 in
+    // none; 1/64 and 1/96 cost more per phase.
     long long eps = std::max<long long>(1, maxc * mult);
+    {
+        long long D = 48;
+        if (const char* fd = std::getenv("KS_FINAL_DIV")) D = std::max(0LL, std::atoll(fd));
+        if (D > 0 && use_pr && maxc > 0) {
+            long long e = std::max<long long>(1, (mult - 1) / D);
+            const long long lo = std::max<long long>(1, eps / ((long long)alpha * alpha));
+            while (e < lo && e <= (1LL << 58) / alpha) e *= alpha;
+            eps = e * alpha;   // the loop divides before each phase
+            pr_div = D;
+        }
+    }
     uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0, early_exits = 0;
     double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
     int phases = 0;
@@ -3627,7 +3648,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         ++phases;
         KS_CHECK(set_eps(eps));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, phases == 1 && use_warm ? warm_thr : 0LL);
+        // After a failed refinement the flow is feasible and ε-optimal at the old ε:
+        // saturating only the arcs that violate the new ε (rc < −ε) is a valid start
+        // (push-relabel at ε needs an ε-optimal pseudoflow, not a 0-optimal one) and
+        // disturbs far less than saturating every negative arc.
+        const long long sat_thr = phases == 1 && use_warm ? warm_thr : (pr_failed && pr_fail_thr ? eps : 0LL);
+        pr_failed = false;
+        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, sat_thr);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         uint64_t phase_sweeps = 0;
         int gi = gi_base;     // sweeps in the next cycle (fewer in a phase's tail, where walks augment)
@@ -3739,6 +3766,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             int rc = price_refine(1, &used, pr_cap);
             if (rc < 0) return rc;
             if (rc == 1) eps = 1;
+            else pr_failed = true;
         }
     } while (eps > 1);
 
