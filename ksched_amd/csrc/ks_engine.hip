@@ -40,6 +40,10 @@
 //              inbox; hub chunks claim excess with a CAS and the last-arriving
 //              chunk finalises the relabel. Bellman-Ford relaxations into a hub
 //              are min-reduced in LDS per workgroup.
+//   tail       once an update leaves ≤ 64 nodes with excess, each sends its
+//              units down the update's distances to a deficit in one kernel
+//              (k_augment walks; k_aug_hub hands a hub's excess on in parallel)
+//              instead of one hop per sweep over dozens of update cycles.
 //   verify     on-device: conservation, capacity, and 1-optimality of the final
 //              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
 //              the total cost is reduced in int64.
@@ -1928,7 +1932,8 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
     for (int step = 0; step < AUG_STEPS; ++step) {
         int b0, en;
         seg_of(g.p0, u, b0, en);
-        // the admissible residual arc of least d(w) ≤ d(u) (ties: lowest position)
+        // the qualifying residual arc (rc ≤ slack·ε; d(w) < d(u), or d(w) = d(u) and
+        // rc < 0) of least d(w) (ties: lowest position)
         long long bd = INF64;
         int ba = -1;
         for (int base = b0; base < en; base += WAVE) {
