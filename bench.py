@@ -106,6 +106,24 @@ def roofline_of(results):
     return line
 
 
+GOLDEN_FILE = os.path.join(ROOT, "tests", "golden", "goldens.json")
+
+
+def golden_of(T, M, R, J, seed):
+    """(cost, flow) of a committed golden (networkx network_simplex, generated in the
+    build container by tests/golden/gen_goldens.py), or None."""
+    if not os.path.exists(GOLDEN_FILE):
+        return None
+    for e in json.load(open(GOLDEN_FILE))["graphs"]:
+        if e.get("family") == "quincy" and list(e.get("params", [])) == [T, M, R, J] and e.get("seed") == seed:
+            return int(e["cost"]), int(e["flow"])
+    return None
+
+
+class ParityError(RuntimeError):
+    pass
+
+
 def timed_cpu(fn, reps: int = 5, warmup: int = 1, pin: bool = True):
     """BASELINE.md §3-4 protocol for a CPU baseline: `warmup` untimed runs, then the
     median of `reps` timed runs, the calling thread pinned to one core (taskset-like,
@@ -251,8 +269,19 @@ def run_full(args, D):
                   "scheduled": int((out > 0).sum().item())}
 
     costs = sorted({r.cost for r in results})
+    flows = sorted({r.flow for r in results})
     cpu = None
-    parity = {"gpu_costs": costs, "flow": results[-1].flow}
+    parity = {"gpu_costs": costs, "flow": results[-1].flow, "steps_checked": len(results)}
+    problems = []
+    if len(costs) != 1:
+        problems.append(f"timed solves disagree on the cost: {costs}")
+    if flows != [T]:
+        problems.append(f"flow value {flows} != {T} tasks")
+    gold = golden_of(T, M, R, J, seed + D.rank)
+    if gold is not None:
+        parity["golden"] = {"cost": gold[0], "flow": gold[1], "source": "tests/golden/goldens.json"}
+        if costs != [gold[0]] or flows != [gold[1]]:
+            problems.append(f"cost/flow {costs}/{flows} != golden {gold}")
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from oracle import ko
         med, ts, out, core = timed_cpu(lambda: ko.reference_path(g), reps=args.cpu_reps)
@@ -267,8 +296,12 @@ def run_full(args, D):
                "pinned_core": core, "phases_ms": [round(x, 1) for x in ms],
                "strong_cpu_cost_scaling": {"value": round(g.m / med2, 1), "unit": "arcs/s", "ms": round(1e3 * med2, 1),
                                            "median_of": len(ts2), "cores": 1}}
-        parity.update({"cpu_cost": ccost, "cpu_flow": cflow, "cs_cost": cs_cost,
-                       "match": costs == [ccost] == [cs_cost] and results[-1].flow == cflow})
+        parity.update({"cpu_cost": ccost, "cpu_flow": cflow, "cs_cost": cs_cost})
+        if not (costs == [ccost] == [cs_cost] and flows == [cflow] and st == 0 and st2 == 0):
+            problems.append(f"GPU {costs}/{flows} vs CPU SSP {ccost}/{cflow} and cost scaling {cs_cost}")
+    parity["match"] = not problems
+    if problems:
+        parity["problems"] = problems
     config = {"workload": f"{args.config}: Quincy-shaped cell graph T={T} M={M} R={R} J={J} "
                           f"(n={g.n}, m={g.m}), step = full device re-solve + device task->PU extraction "
                           f"(Solve() -> TaskMapping), one graph per GPU",
@@ -283,37 +316,73 @@ def run_full(args, D):
 
 # -------------------------------------------------------------- incremental
 def run_incremental(args, D):
+    """Config 4: the config-3 cell solved, then `steps` timed
+    churn rounds after `warmup` untimed ones. A round = ks_apply_deltas (in HBM)
+    + ks_solve + the task mapping. Rank 0 at N = 1 replays the same rounds through
+    the CPU restatement of the reference's incremental mode (the change block as
+    text, Flowlessly-style incremental SSP from the previous round's flow and
+    potentials, f lines, BFS mapping), with the cold SSP reference path beside it,
+    and checks every round's cost and flow against it (outside the timed region)."""
     T, M, R, J, seed = gen.CONFIGS["config3"]
     cell = churn.Cell(T, M, R, J, seed + D.rank)
     ctx = native.Context(D.local, **dict(opts_of(args), warm_start=args.warm))
-    ctx.load_graph(cell.graph())
+    g = cell.graph()
+    ctx.load_graph(g)
     r0 = ctx.solve()
     mp = ctx.task_mapping()
     done = arrive = T // 20
-    rounds = []
-    results = []
+    rounds, results = [], []
     t_total = 0.0
+    problems = []
+    cpu_on = D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto"
+    inc = cold_ms = inc_ms = None
+    if cpu_on:
+        from oracle import ko
+        inc = ko.IncrementalSSP()
+        t0 = time.perf_counter()
+        st, c, f, _ = inc.round(g)                      # the daemon's first (full) solve
+        inc_first_ms = 1e3 * (time.perf_counter() - t0)
+        if (c, f) != (r0.cost, r0.flow):
+            problems.append(f"initial solve: GPU {r0.cost}/{r0.flow} vs CPU {c}/{f}")
+        cold_ms, inc_ms = [], []
     for i in range(args.warmup + args.steps):
         d = cell.step(mp, done=done, arrive=arrive)
+        fresh = list(cell.last_arrived_ids)
         D.sync()
         ts = time.perf_counter()
         ctx.apply_deltas(d)
         ta = time.perf_counter()
-        sst = ctx.store_stats()
         r = ctx.solve()
         tb = time.perf_counter()
         mp = ctx.task_mapping()
         te = time.perf_counter()
         D.sync()
         dt = D.max(time.perf_counter() - ts)
-        rec = {"round": i + 1, "deltas": int(d.shape[0]), "ms": round(1e3 * dt, 3),
+        sst = ctx.store_stats()
+        rec = {"round": i + 1, "timed": i >= args.warmup, "deltas": int(d.shape[0]), "ms": round(1e3 * dt, 3),
                "apply_ms": round(1e3 * (ta - ts), 3), "solve_ms": round(1e3 * (tb - ta), 3),
                "mapping_ms": round(1e3 * (te - tb), 3), "cost": r.cost, "flow": r.flow,
                "warm": r.raw["warm_started"], "phases": r.raw["phases"], "sweeps": r.raw["sweeps"],
                "updates": r.raw["global_updates"], "bf_rounds": r.raw["gu_iterations"],
+               "recoveries": r.raw["recoveries"],
                "solve_parts_ms": {k: round(v, 2) for k, v in r.raw["ms"].items()},
                "m": r.raw["n_arcs"], "running": int((cell.state == cell.RUN).sum()),
-               "rebuilt": r.raw["rebuilt"], "store": {k: sst[k] for k in ("inserted", "updated", "killed", "superseded")}}
+               "rebuilt": r.raw["rebuilt"], "rebuilds_since_load": sst["rebuilds"],
+               "store": {k: sst[k] for k in ("inserted", "updated", "killed", "superseded")}}
+        if r.flow != cell.graph().supply[cell.graph().supply > 0].sum():
+            problems.append(f"round {i + 1}: flow {r.flow} short of the supply")
+        if cpu_on:
+            g = cell.graph()
+            t0 = time.perf_counter()
+            st, c, f, _ = inc.round(g, d, fresh)
+            inc_ms.append(1e3 * (time.perf_counter() - t0))
+            t0 = time.perf_counter()
+            st2, c2, f2, _, _ = ko.reference_path(g)
+            cold_ms.append(1e3 * (time.perf_counter() - t0))
+            rec["cpu"] = {"incremental_ms": round(inc_ms[-1], 1), "cold_ms": round(cold_ms[-1], 1), "cost": c,
+                          "incremental_phases_ms": {k: round(v, 1) for k, v in inc.last["ms"].items()}}
+            if not ((r.cost, r.flow) == (c, f) == (c2, f2) and st == st2 == 0):
+                problems.append(f"round {i + 1}: GPU {r.cost}/{r.flow} vs CPU incremental {c}/{f}, cold {c2}/{f2}")
         if i >= args.warmup:
             t_total += dt
             results.append(r)
@@ -321,24 +390,34 @@ def run_incremental(args, D):
     ms_per_step = 1e3 * t_total / max(1, args.steps)
     m_avg = sum(r.raw["n_arcs"] for r in results) / max(1, len(results))
     value = D.world * m_avg / (ms_per_step / 1e3)
-    parity = None
+    timed = [x for x in rounds if x["timed"]]
+    parity = {"rounds_checked": len(rounds) if cpu_on else 0, "flows_checked": len(rounds),
+              "match": not problems, "last_round_gpu_cost": rounds[-1]["cost"]}
+    if problems:
+        parity["problems"] = problems
     cpu = None
-    if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
-        from oracle import ko
-        g = cell.graph()
-        med, ts, out, core = timed_cpu(lambda: ko.reference_path(g), reps=args.cpu_reps)
-        st, ccost, cflow, _, ms = out
-        cpu = {"value": round(g.m / med, 1), "unit": "arcs/s", "cores": 1, "kind": "port",
-               "sample": f"the last round's full graph through the restatement of the reference CPU path (export "
-                         f"-> SSP -> f lines -> BFS), median of {len(ts)} after 1 warm-up, pinned to core {core}",
-               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts),
-               "pinned_core": core}
-        parity = {"last_round_gpu_cost": rounds[-1]["cost"], "cpu_cost": ccost, "cpu_flow": cflow,
-                  "match": rounds[-1]["cost"] == ccost and rounds[-1]["flow"] == cflow}
+    if cpu_on:
+        ti = [x for x, rr in zip(inc_ms, rounds) if rr["timed"]]
+        tc = [x for x, rr in zip(cold_ms, rounds) if rr["timed"]]
+        med_i, med_c = float(np.median(ti)), float(np.median(tc))
+        cpu = {"value": round(m_avg / (med_i / 1e3), 1), "unit": "arcs/s", "cores": 1, "kind": "port",
+               "sample": f"the same {len(ti)} timed rounds through the restatement of the reference's incremental mode "
+                         f"(ExportIncremental text -> parse -> incremental SSP from the previous round's flow and "
+                         f"potentials -> f lines -> BFS mapping; Flowlessly daemon, solver.go:30-34,86-89), median "
+                         f"per round, 1 thread",
+               "ms": round(med_i, 1), "times_ms": [round(x, 1) for x in ti], "first_full_solve_ms": round(inc_first_ms, 1),
+               "cold_reference_path": {"value": round(m_avg / (med_c / 1e3), 1), "unit": "arcs/s", "ms": round(med_c, 1),
+                                       "times_ms": [round(x, 1) for x in tc], "cores": 1,
+                                       "sample": "each timed round's full graph through the cold reference path "
+                                                 "(export -> SSP -> f lines -> BFS), median"}}
     config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
                           f"{arrive} arrivals per round, pins/ageing/capacity deltas; step = apply deltas + "
-                          f"{'warm-started' if args.warm else 'from-scratch'} re-solve + mapping", "tasks": T, "machines": M, "seed": seed,
-              "initial_solve_ms": round(r0.raw["ms"]["total"], 3), "parallelism": f"independent cells x{D.world}"}
+                          f"{'warm-started' if args.warm else 'from-scratch'} re-solve + mapping; {args.steps} timed "
+                          f"rounds after {args.warmup}", "tasks": T, "machines": M, "seed": seed,
+              "initial_solve_ms": round(r0.raw["ms"]["total"], 3), "rounds": args.steps,
+              "round_ms": {"median": round(float(np.median([x["ms"] for x in timed])), 3),
+                           "max": round(max(x["ms"] for x in timed), 3)},
+              "parallelism": f"independent cells x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, rounds=rounds, roofline=roofline_of(results),
                      cpu_baseline=cpu, parity=parity)
     ctx.close()
@@ -429,6 +508,13 @@ def run_batch(args, D):
             per_graph = np.asarray([r.cost for r in results[-len(ctxs):]], np.int64)
     cpu = None
     parity = {"total_cost": int(per_graph.sum()) if per_graph is not None else None}
+    if args.batch_mode == "streams":   # per-cell solve latency (each context's own solve)
+        cell_ms = [r.raw["ms"]["total"] for r in results[-len(ctxs):]]
+        extra_cells = {"median_ms": round(float(np.median(cell_ms)), 3), "max_ms": round(max(cell_ms), 3),
+                       "min_ms": round(min(cell_ms), 3), "cells": len(cell_ms),
+                       "note": "host wall time of each context's ks_solve while the cells ran concurrently"}
+    else:
+        extra_cells = None
     if D.rank == 0 and D.world == 1 and args.cpu_baseline == "auto":
         from concurrent.futures import ThreadPoolExecutor
         from oracle import ko
@@ -447,6 +533,8 @@ def run_batch(args, D):
                "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts)}
         parity.update({"checked_graphs": num,
                        "match": bool(per_graph is not None and all(o[1] == int(c) for o, c in zip(outs, per_graph)))})
+        if not parity["match"]:
+            parity["problems"] = ["a graph's GPU cost differs from the CPU reference path"]
     mode = {"abi": "C-ABI batch (union per device, RCCL gather inside libksmcmf)",
             "union": "one device solve of their disjoint union",
             "streams": f"one context each, solved concurrently ({args.workers} workers/GPU)"}[args.batch_mode]
@@ -456,7 +544,7 @@ def run_batch(args, D):
               "parallelism": f"graph sharding x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
                      roofline=roofline_of(results), cpu_baseline=cpu, gather=gather, parity=parity,
-                     solve=dict(results[-1].raw))
+                     cell_latency=extra_cells, solve=dict(results[-1].raw))
     if args.batch_mode == "abi":
         bt.close()
     else:
@@ -473,8 +561,8 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 5; incremental: 10 rounds)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; incremental: 1)")
     ap.add_argument("--workload", default="full", choices=["full", "incremental", "batch"])
     ap.add_argument("--config", default="config3", choices=sorted(gen.CONFIGS))
     ap.add_argument("--graphs", type=int, default=64)
@@ -487,13 +575,24 @@ def main():
     ap.add_argument("--gu-interval", type=int, default=0)
     ap.add_argument("--price-refine", type=int, default=-1)
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 10 if args.workload == "incremental" else 5    # config 4 is 10 rounds
+    if args.warmup is None:
+        args.warmup = 1 if args.workload == "incremental" else 2
 
     D = Dist()
     run = {"full": run_full, "incremental": run_incremental, "batch": run_batch}[args.workload]
     line = run(args, D)
+    # the exit status doubles as a correctness gate: any rank whose solves disagree
+    # with the golden / CPU reference / each other fails the run (after the line)
+    ok = bool((line.get("parity") or {}).get("match", True))
+    bad = D.max(0.0 if ok else 1.0) > 0
     if D.rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     D.close()
+    if bad:
+        print("bench.py: PARITY FAILURE: " + json.dumps((line.get("parity") or {}).get("problems")), file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define KSMCMF_ABI_VERSION 1
+#define KSMCMF_ABI_VERSION 2   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls */
 
 /* status codes (0 = OK) */
 #define KS_OK            0
@@ -93,7 +93,28 @@ typedef struct ks_opts {
     int32_t  warm_start;       /* 1: re-solve from the previous flow and prices after
                                   ks_apply_deltas; 0 (default): every solve from
                                   scratch (faster on config 4)      */
-    int32_t  reserved[10];
+    /* solver tuning; 0 selects the library default given in brackets.
+       None of these changes the result — only how fast it is reached. */
+    int32_t  walk_slack;       /* a phase's tail walks take residual arcs of reduced cost
+                                  ≤ walk_slack·ε while ε > 1 [4]; < 0 disables the walks */
+    int32_t  final_div;        /* the phase price refinement certifies runs at 1/final_div
+                                  of a cost unit [48]; < 0: the plain max|cost|/α^k ladder */
+    int32_t  pr_rounds;        /* Bellman-Ford rounds one price refinement may take [160] */
+    int32_t  phase_exit;       /* a coarse phase ends once ≤ phase_exit nodes hold excess
+                                  [256] ... */
+    int32_t  phase_frac;       /* ... and ≤ 1/phase_frac of the phase's peak [128]; < 0 in
+                                  phase_exit: coarse phases always drain completely   */
+    int32_t  tail_sweeps;      /* sweeps per cycle once ≤ 64 nodes hold excess [4]      */
+    int32_t  bf_margin;        /* Bellman-Ford rounds enqueued per cycle beyond the last
+                                  update's count [6]                                    */
+    int32_t  two_hop;          /* Bellman-Ford relaxes a task's / PU's in-arcs in the round
+                                  its distance dropped [1]; < 0 off                     */
+    int32_t  log_cycles;       /* 1: one diagnostic line per update cycle on stderr [0] */
+    int32_t  fault_inject;     /* TESTS ONLY [0]: bit 0 — the last phase's walks use the
+                                  coarse slack at ε = 1 (may end non-1-optimal); bit 1 —
+                                  the final prices are perturbed before verification.
+                                  Both must be repaired by the certificate recovery.    */
+    int32_t  reserved[8];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */
@@ -155,6 +176,10 @@ typedef struct ks_result {
     int32_t  warm_started;     /* 1 when this solve started from the previous solution   */
     int32_t  rebuilt;          /* 1 when this solve rebuilt the residual CSR from the arc
                                   table (after a load, or a delta that did not fit)     */
+    int32_t  recoveries;       /* times the final optimality certificate failed and was
+                                  repaired (price refinement, else one more ε = 1 phase
+                                  from the current flow) before the solve returned      */
+    int32_t  _pad;
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */
@@ -317,8 +342,21 @@ int ks_batch_solve(ks_batch* b, ks_result* results);
 /* Collective (all ranks call it): per graph its cost, flow value and the PU node id
  * (local to the graph, 0 = unscheduled) of each of its task nodes in id order,
  * gathered to global rank 0, whose pu[g·max_tasks ..], cost[g], flow[g] receive
- * them (other ranks may pass NULL). */
+ * them (other ranks may pass NULL). A rank that fails to pack its rows still
+ * enters the collective; every rank then returns that failure. */
 int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, int64_t* flow);
+
+/* Layout of the gather (host-only, no device or RCCL: the packing and unpacking
+ * of ks_batch_gather use exactly these). Graph g is owned by global rank
+ * g mod world as its (g div world)-th graph; each rank sends one block of
+ * ks_batch_block_len elements: [status][slots rows of 2 + max_tasks: cost, flow
+ * value, PU per task]. ks_batch_unpack turns the world blocks rank 0 received (in
+ * rank order) into graph order; it returns a rank's non-zero status word. */
+size_t      ks_batch_slots(size_t ngraphs, int world);
+int         ks_batch_owner(size_t g, int world, int* rank, size_t* slot);
+size_t      ks_batch_block_len(size_t ngraphs, int world, size_t max_tasks);
+int         ks_batch_unpack(const int64_t* gathered, size_t ngraphs, int world, size_t max_tasks, uint64_t* pu,
+                            int64_t* cost, int64_t* flow);
 
 #ifdef __cplusplus
 }

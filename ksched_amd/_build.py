@@ -30,18 +30,51 @@ def stale() -> bool:
     return any(os.path.getmtime(p) > t for p in DEPS)
 
 
+OBJ_DIR = os.path.join(HERE, "build")
+HEADERS = [p for p in DEPS if p.endswith(".h")]
+
+
+def _flags(arch: str, defines=()) -> list[str]:
+    return [f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+            "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
+
+
+def _compile_all(arch: str, tag: str, defines=(), force: bool = False, verbose: bool = False) -> list[str]:
+    """One object per source, compiled in parallel (a source is rebuilt when it or
+    any header is newer than its object)."""
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    jobs = []
+    for src in SOURCES:
+        obj = os.path.join(OBJ_DIR, f"{tag}_{os.path.basename(src)}.o")
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
+            jobs.append((src, obj))
+    def run(job):
+        src, obj = job
+        cmd = [hipcc(), *_flags(arch, defines), "-c", src, "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+    with ThreadPoolExecutor(max(1, min(len(jobs), os.cpu_count() or 1))) as ex:
+        list(ex.map(run, jobs))
+    return [os.path.join(OBJ_DIR, f"{tag}_{os.path.basename(src)}.o") for src in SOURCES]
+
+
+def _link(objs: list[str], arch: str, out: str, verbose: bool = False):
+    cmd = [hipcc(), f"--offload-arch={arch}", "-shared", "-fPIC", *objs, "-ldl", "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not stale():
         return LIB
     arch = os.environ.get("KS_OFFLOAD_ARCH", "gfx950")
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"),
-           *SOURCES, "-ldl", "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    _link(_compile_all(arch, "lib", force=force, verbose=verbose), arch, LIB, verbose)
     return LIB
 
 
@@ -68,11 +101,7 @@ def variant_path(tag: str) -> str:
 def build_variant(tag: str, defines: list[str]) -> str:
     """An extra copy of the library compiled with -D<defines> (tuning experiments)."""
     out = variant_path(tag)
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines],
-           *SOURCES, "-ldl", "-o", out + ".tmp"]
-    subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    _link(_compile_all("gfx950", "v_" + tag, defines, force=True), "gfx950", out)
     return out
 
 

@@ -76,6 +76,7 @@ class Cell:
         self.n_slots = T
         self.round = 0
         self.initial = g
+        self.last_arrived_ids: list[int] = []   # task ids (re)created by the last step
 
     # ----------------------------------------------------------------- views
     def _grow(self, need: int):
@@ -192,6 +193,7 @@ class Cell:
 
         # 3. arrivals (FIFO id reuse, then fresh ids)
         arrived = []
+        self.last_arrived_ids = []
         if arrive:
             x = gen.stream(seed, 1 << 32, 9 * arrive).reshape(arrive, 9)
             J, R = self.J, self.R
@@ -220,6 +222,7 @@ class Cell:
                 self.job[si] = j[a]
                 self.adst[si] = dsts[a]
                 self.acost[si] = costs[a]
+                self.last_arrived_ids.append(ti)
                 out.append((KS_ADD_NODE, 1, ti, 0, 0, 0, 0, 0, 0, 1))
                 for d, c in zip(dsts[a].tolist(), costs[a].tolist()):
                     out.append((KS_ADD_ARC, 0, 0, ti, d, 0, 1, c, 0, 0))

@@ -39,6 +39,8 @@ struct Rccl {
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
 
     bool load(std::string& err) {
@@ -64,6 +66,7 @@ struct Rccl {
         sym(GroupEnd, "ncclGroupEnd");
         sym(Send, "ncclSend");
         sym(Recv, "ncclRecv");
+        sym(AllReduce, "ncclAllReduce");
         sym(GetErrorString, "ncclGetErrorString");
         if (!ok) err = "RCCL is missing a symbol";
         return ok;
@@ -75,11 +78,24 @@ Rccl& rccl() {
     return r;
 }
 
+// ---- row layout of ks_batch_gather (host code, shared by the packing, the
+// unpacking and the CPU tests through the exported ks_batch_* layout calls) ----
+// Graph g lives on global rank g mod world, as that rank's (g div world)-th
+// graph. Every rank sends ONE block: [status word][slots rows], a row being
+// [cost, flow value, PU id of each task (cell-local, 0 = unscheduled), padded to
+// max_tasks]. Rank 0 receives the blocks in rank order.
+inline size_t kb_slots(size_t ngraphs, int world) { return (ngraphs + (size_t)world - 1) / (size_t)std::max(1, world); }
+inline size_t kb_rowlen(size_t max_tasks) { return 2 + max_tasks; }
+inline size_t kb_block(size_t ngraphs, int world, size_t max_tasks) {
+    return 1 + std::max<size_t>(1, kb_slots(ngraphs, world)) * kb_rowlen(max_tasks);
+}
+inline size_t kb_row_in_block(size_t slot, size_t max_tasks) { return 1 + slot * kb_rowlen(max_tasks); }
+
 // row r: PU ids of its tasks made cell-local (subtract the cell's node offset)
 __global__ void k_localize(int rows, int rowlen, const long long* __restrict__ off, long long* __restrict__ buf) {
     const int r = blockIdx.y;
     if (r >= rows) return;
-    long long* row = buf + (size_t)r * rowlen;
+    long long* row = buf + 1 + (size_t)r * rowlen;
     for (int i = 2 + blockIdx.x * blockDim.x + threadIdx.x; i < rowlen; i += gridDim.x * blockDim.x)
         if (row[i] > 0) row[i] -= off[r];
 }
@@ -97,6 +113,7 @@ struct ks_batch {
         std::vector<int64_t> toff;      // task offset of each graph in the dense task vector (+ total)
         long long* rows = nullptr;      // device: graphs.size() × rowlen
         long long* scratch = nullptr;   // device: dense task→PU vector, offsets
+        long long* stat = nullptr;      // device: this rank's status word for the status all-reduce
         size_t rows_cap = 0, scratch_cap = 0;
         ks_result res{};
     };
@@ -149,6 +166,37 @@ ks_batch* make_batch(int world, const ks_opts* opts, const std::vector<std::pair
 
 extern "C" {
 
+size_t ks_batch_slots(size_t ngraphs, int world) { return world < 1 ? 0 : kb_slots(ngraphs, world); }
+
+int ks_batch_owner(size_t g, int world, int* rank, size_t* slot) {
+    if (world < 1 || !rank || !slot) return KS_E_INVALID;
+    *rank = (int)(g % (size_t)world);
+    *slot = g / (size_t)world;
+    return KS_OK;
+}
+
+size_t ks_batch_block_len(size_t ngraphs, int world, size_t max_tasks) {
+    return world < 1 ? 0 : kb_block(ngraphs, world, max_tasks);
+}
+
+int ks_batch_unpack(const int64_t* gathered, size_t ngraphs, int world, size_t max_tasks, uint64_t* pu,
+                    int64_t* cost, int64_t* flow) {
+    if (!gathered || world < 1) return KS_E_INVALID;
+    const size_t block = kb_block(ngraphs, world, max_tasks);
+    for (int r = 0; r < world; ++r)
+        if (gathered[(size_t)r * block] != 0) return (int)gathered[(size_t)r * block];   // a rank's status
+    for (size_t g = 0; g < ngraphs; ++g) {
+        int r = 0;
+        size_t slot = 0;
+        ks_batch_owner(g, world, &r, &slot);
+        const int64_t* row = gathered + (size_t)r * block + kb_row_in_block(slot, max_tasks);
+        if (cost) cost[g] = row[0];
+        if (flow) flow[g] = row[1];
+        if (pu) std::memcpy(pu + g * max_tasks, row + 2, max_tasks * sizeof(uint64_t));
+    }
+    return KS_OK;
+}
+
 int ks_batch_unique_id(uint8_t* id) {
     std::string err;
     if (!id || !rccl().load(err)) return KS_E_DEVICE;
@@ -195,6 +243,7 @@ void ks_batch_destroy(ks_batch* b) {
         if (l.comm) rccl().CommDestroy(l.comm);
         if (l.rows) (void)hipFree(l.rows);
         if (l.scratch) (void)hipFree(l.scratch);
+        if (l.stat) (void)hipFree(l.stat);
         ks_destroy(l.ctx);
     }
     if (b->root_buf) {
@@ -213,7 +262,12 @@ int ks_batch_load(ks_batch* b, size_t ngraphs, const ks_node* const* nodes, cons
     b->ngraphs = ngraphs;
     for (auto& l : b->loc) {
         l.graphs.clear();
-        for (size_t g = (size_t)l.grank; g < ngraphs; g += (size_t)b->world) l.graphs.push_back((int)g);
+        for (size_t g = 0; g < ngraphs; ++g) {
+            int r = 0;
+            size_t slot = 0;
+            ks_batch_owner(g, b->world, &r, &slot);
+            if (r == l.grank) l.graphs.push_back((int)g);   // slot = its index in l.graphs
+        }
         if (l.graphs.size() > 1024) return b->fail(KS_E_INVALID, "more than 1024 graphs on one device");
         // the disjoint union of this device's graphs: node ids offset per graph
         std::vector<ks_node> un;
@@ -232,6 +286,11 @@ int ks_batch_load(ks_batch* b, size_t ngraphs, const ks_node* const* nodes, cons
             }
             for (size_t i = 0; i < m[g]; ++i) {
                 ks_arc a = arcs[g][i];
+                // an arc must stay inside its own graph: past its max id it would land
+                // on a node of the next graph in the union and couple two cells
+                if (a.src == 0 || a.dst == 0 || a.src > maxid || a.dst > maxid)
+                    return b->fail(KS_E_INVALID, "graph " + std::to_string(g) + ": arc " + std::to_string(a.src) +
+                                                     "->" + std::to_string(a.dst) + " outside its node id range");
                 a.src += (uint64_t)l.off.back();
                 a.dst += (uint64_t)l.off.back();
                 ua.push_back(a);
@@ -261,19 +320,20 @@ int ks_batch_solve(ks_batch* b, ks_result* results) {
 
 int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, int64_t* flow) {
     if (!b) return KS_E_INVALID;
-    const size_t rowlen = 2 + max_tasks;
-    const size_t slots = (b->ngraphs + b->world - 1) / std::max(1, b->world);
-    const size_t block = std::max<size_t>(1, slots) * rowlen;   // elements per rank
+    const size_t rowlen = kb_rowlen(max_tasks);
+    const size_t block = kb_block(b->ngraphs, b->world, max_tasks);   // elements per rank
     bool has_root = false;
-    // 1. every device packs its rows: [cost, flow value, cell-local PU per task]
-    for (auto& l : b->loc) {
+    // 1. every device packs its block: [status][rows: cost, flow value, cell-local PU per task].
+    //    A rank that fails here still takes part in the collective below (with its
+    //    status word set), so its peers never wait for a send that is not posted.
+    std::vector<int> status(b->loc.size(), KS_OK);
+    std::string first_err;
+    for (size_t li = 0; li < b->loc.size(); ++li) {
+        auto& l = b->loc[li];
         KB_HIP(hipSetDevice(l.device));
         if (l.grank == 0) has_root = true;
         ks_ctx* c = l.ctx;
         const size_t k = l.graphs.size();
-        for (size_t i = 0; i < k; ++i)
-            if ((size_t)(l.toff[i + 1] - l.toff[i]) > max_tasks)
-                return b->fail(KS_E_INVALID, "a graph has more tasks than max_tasks");
         hipStream_t st = c->eng.stream();
         if (l.rows_cap < block) {
             if (l.rows) (void)hipFree(l.rows);
@@ -281,39 +341,81 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
             KB_HIP(hipMalloc(&l.rows, block * sizeof(long long)));
             l.rows_cap = block;
         }
+        KB_HIP(hipMemsetAsync(l.rows, 0, block * sizeof(long long), st));
+        int rc = KS_OK;
+        for (size_t i = 0; i < k && rc == KS_OK; ++i)
+            if ((size_t)(l.toff[i + 1] - l.toff[i]) > max_tasks) {
+                rc = KS_E_INVALID;
+                c->err = "a graph has more tasks than max_tasks";
+            }
         const size_t need = (size_t)l.toff.back() + 3 * (k + 1);
-        if (l.scratch_cap < need) {
+        if (rc == KS_OK && l.scratch_cap < need) {
             if (l.scratch) (void)hipFree(l.scratch);
             l.scratch = nullptr;
             KB_HIP(hipMalloc(&l.scratch, std::max<size_t>(need, 1) * sizeof(long long)));
             l.scratch_cap = need;
         }
-        KB_HIP(hipMemsetAsync(l.rows, 0, block * sizeof(long long), st));
-        if (!k) continue;
-        long long* dcost = l.scratch + l.toff.back();
-        long long* dflow = dcost + (k + 1);
-        long long* doff = dflow + (k + 1);
-        int rc = c->eng.cell_sums(l.off.data(), k, (int64_t*)dcost, (int64_t*)dflow, c->err);
-        size_t cnt = 0;
-        if (rc == KS_OK) rc = ks_get_task_pu_device(c, (uint64_t*)l.scratch, (size_t)l.toff.back(), &cnt);
-        if (rc) return b->fail(rc, ks_last_error(c));
-        KB_HIP(hipMemcpy2DAsync(l.rows, rowlen * sizeof(long long), dcost, sizeof(long long), sizeof(long long), k,
-                                hipMemcpyDeviceToDevice, st));
-        KB_HIP(hipMemcpy2DAsync(l.rows + 1, rowlen * sizeof(long long), dflow, sizeof(long long), sizeof(long long), k,
-                                hipMemcpyDeviceToDevice, st));
-        for (size_t i = 0; i < k; ++i) {
-            const size_t t = (size_t)(l.toff[i + 1] - l.toff[i]);
-            if (t)
-                KB_HIP(hipMemcpyAsync(l.rows + i * rowlen + 2, l.scratch + l.toff[i], t * sizeof(long long),
-                                      hipMemcpyDeviceToDevice, st));
+        if (rc == KS_OK && k) {
+            long long* dcost = l.scratch + l.toff.back();
+            long long* dflow = dcost + (k + 1);
+            long long* doff = dflow + (k + 1);
+            rc = c->eng.cell_sums(l.off.data(), k, (int64_t*)dcost, (int64_t*)dflow, c->err);
+            size_t cnt = 0;
+            if (rc == KS_OK) rc = ks_get_task_pu_device(c, (uint64_t*)l.scratch, (size_t)l.toff.back(), &cnt);
+            if (rc == KS_OK) {
+                long long* rows = l.rows + kb_row_in_block(0, max_tasks);
+                KB_HIP(hipMemcpy2DAsync(rows, rowlen * sizeof(long long), dcost, sizeof(long long), sizeof(long long),
+                                        k, hipMemcpyDeviceToDevice, st));
+                KB_HIP(hipMemcpy2DAsync(rows + 1, rowlen * sizeof(long long), dflow, sizeof(long long),
+                                        sizeof(long long), k, hipMemcpyDeviceToDevice, st));
+                for (size_t i = 0; i < k; ++i) {
+                    const size_t t = (size_t)(l.toff[i + 1] - l.toff[i]);
+                    if (t)
+                        KB_HIP(hipMemcpyAsync(l.rows + kb_row_in_block(i, max_tasks) + 2, l.scratch + l.toff[i],
+                                              t * sizeof(long long), hipMemcpyDeviceToDevice, st));
+                }
+                KB_HIP(hipMemcpyAsync(doff, l.off.data(), k * sizeof(long long), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_localize, dim3(std::max<size_t>(1, std::min<size_t>(64, (rowlen + 255) / 256)), k),
+                                   dim3(256), 0, st, (int)k, (int)rowlen, (const long long*)doff, l.rows);
+                KB_HIP(hipGetLastError());
+            }
         }
-        KB_HIP(hipMemcpyAsync(doff, l.off.data(), k * sizeof(long long), hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_localize, dim3(std::max<size_t>(1, std::min<size_t>(64, (rowlen + 255) / 256)), k),
-                           dim3(256), 0, st, (int)k, (int)rowlen, (const long long*)doff, l.rows);
-        KB_HIP(hipGetLastError());
+        if (rc != KS_OK) {
+            status[li] = rc;
+            if (first_err.empty()) first_err = "rank " + std::to_string(l.grank) + ": " + c->err;
+            const long long sw = rc;
+            KB_HIP(hipMemcpyAsync(l.rows, &sw, sizeof(long long), hipMemcpyHostToDevice, st));
+        }
         KB_HIP(hipStreamSynchronize(st));
     }
-    // 2. one group: every rank's rows to global rank 0
+    // 2. every rank learns whether any rank failed (min over the status words), so
+    //    all of them return the same error instead of only the failing one
+    if (b->world > 1) {
+        for (size_t li = 0; li < b->loc.size(); ++li) {
+            auto& l = b->loc[li];
+            KB_HIP(hipSetDevice(l.device));
+            if (!l.stat) KB_HIP(hipMalloc(&l.stat, sizeof(long long)));
+            const long long sw = status[li];
+            KB_HIP(hipMemcpy(l.stat, &sw, sizeof(long long), hipMemcpyHostToDevice));
+        }
+        KB_NCCL(rccl().GroupStart());
+        for (auto& l : b->loc)
+            KB_NCCL(rccl().AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream()));
+        KB_NCCL(rccl().GroupEnd());
+        long long worst = 0;
+        for (auto& l : b->loc) {
+            KB_HIP(hipSetDevice(l.device));
+            long long sw = 0;
+            KB_HIP(hipStreamSynchronize(l.ctx->eng.stream()));
+            KB_HIP(hipMemcpy(&sw, l.stat, sizeof(long long), hipMemcpyDeviceToHost));
+            worst = std::min(worst, sw);
+        }
+        if (worst != 0)
+            return b->fail((int)worst, first_err.empty() ? "another rank failed to pack its rows (status " +
+                                                               std::to_string(worst) + ")"
+                                                         : first_err);
+    }
+    // 3. one group: every rank's block to global rank 0
     long long* rbuf = nullptr;
     for (auto& l : b->loc)
         if (l.grank == 0) {
@@ -345,20 +447,18 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
         KB_HIP(hipSetDevice(l.device));
         KB_HIP(hipStreamSynchronize(l.ctx->eng.stream()));
     }
+    for (int rc : status)
+        if (rc != KS_OK) return b->fail(rc, first_err);   // this process's own failure, after the collective
     if (!has_root) return KS_OK;
-    // 3. rank 0: rows back in graph order
+    // 4. rank 0: every rank's status word, then the rows back in graph order
     std::vector<long long> host(block * (size_t)b->world);
     for (auto& l : b->loc)
         if (l.grank == 0) {
             KB_HIP(hipSetDevice(l.device));
             KB_HIP(hipMemcpy(host.data(), rbuf, host.size() * sizeof(long long), hipMemcpyDeviceToHost));
         }
-    for (size_t g = 0; g < b->ngraphs; ++g) {
-        const long long* row = host.data() + (g % b->world) * block + (g / b->world) * rowlen;
-        if (cost) cost[g] = row[0];
-        if (flow) flow[g] = row[1];
-        if (pu) std::memcpy(pu + g * max_tasks, row + 2, max_tasks * sizeof(uint64_t));
-    }
+    const int rc = ks_batch_unpack((const int64_t*)host.data(), b->ngraphs, b->world, max_tasks, pu, cost, flow);
+    if (rc != KS_OK) return b->fail(rc, "a rank failed to pack its rows (status " + std::to_string(rc) + ")");
     return KS_OK;
 }
 

@@ -34,6 +34,7 @@ struct ks_ctx {
     int64_t dev_sink_supply = 0;           // the sink's supply as the device has it
     bool have_solution = false;
     bool flows_fresh = false;
+    bool store_bad = false;                // a load / apply failed on the device: reload first
     std::vector<ks_flow> flows;
 
     int fail(int code, const std::string& msg) {

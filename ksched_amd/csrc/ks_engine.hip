@@ -2013,6 +2013,15 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
     }
 }
 
+// TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
+// the solve, so the certificate fails on an optimal flow and must be repaired.
+__global__ void k_perturb_price(DG g, int x, long long delta) {
+    if (x < g.n) {
+        g.p0[ni(x)] -= delta;
+        g.p1[ni(x)] -= delta;
+    }
+}
+
 // PR success: p ← p − ε·d (d ≤ 0).
 __global__ void k_pr_apply(DG g) {
     if (!g.ctl->bf_done) return;
@@ -2221,7 +2230,7 @@ __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, con
                              const long long* __restrict__ outv, const long long* __restrict__ outs,
                              const long long* __restrict__ inv, const long long* __restrict__ ins,
                              const int* __restrict__ iperm, const unsigned char* __restrict__ itype,
-                             const int* __restrict__ rank, const int* __restrict__ is_task,
+                             const int* __restrict__ rank, const int* __restrict__ is_task, long long cap,
                              unsigned long long* __restrict__ out) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
         if (!is_task[v]) continue;
@@ -2242,7 +2251,7 @@ __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, con
             k = ins[q] - ins[first[y]] + off;
             x = y;
         }
-        out[rank[v]] = last_pu >= 0 ? (unsigned long long)iperm[last_pu] + 1 : 0ULL;
+        if (rank[v] < cap) out[rank[v]] = last_pu >= 0 ? (unsigned long long)iperm[last_pu] + 1 : 0ULL;
     }
 }
 
@@ -3116,7 +3125,7 @@ int Engine::task_pu(uint64_t* dev_out, size_t cap, size_t* count, int64_t n_task
                        (const long long*)s.map_outv.p, (const long long*)s.map_outs.p,
                        (const long long*)s.map_inv.p, (const long long*)s.map_ins.p, (const int*)s.iperm.p,
                        (const unsigned char*)s.map_itype.p, (const int*)s.map_rank.p,
-                       (const int*)s.map_is_task.p, (unsigned long long*)dev_out);
+                       (const int*)s.map_is_task.p, (long long)cap, (unsigned long long*)dev_out);
     KS_CHECK(hipGetLastError());
     KS_CHECK(hipStreamSynchronize(st));
     return KS_OK;
@@ -3428,6 +3437,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     s.solved = false;
     res.warm_started = use_warm ? 1 : 0;
     res.rebuilt = s.csr_valid ? 0 : 1;
+    res.recoveries = 0;
     KS_CHECK(hipEventRecord(s.ev[0], st));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
@@ -3500,7 +3510,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
 
     // ------------------------------------------------------------ phases ---
 #ifdef KS_STAMPS
-    const char* stamp_path = std::getenv("KS_STAMPS_OUT");
+    const char* stamp_path = std::getenv("KS_STAMPS_OUT");   // diagnostic builds only
     if (stamp_path) {
         KS_CHECK(s.stamps.ensure(STAMP_W * 8192));
         std::vector<unsigned long long> init(STAMP_W * 8192, 0);
@@ -3509,42 +3519,33 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipStreamSynchronize(st));
     }
 #endif
+    // Tuning comes from ks_opts only (0 = default; include/ksmcmf.h): nothing in
+    // the environment changes the algorithm.
+    const ks_opts& o = s.opts;
     DG g = s.dg();
-    {
-        const char* ex = std::getenv("KS_EXPAND");   // two hops per round through tasks and PUs
-        g.expand = ex ? std::atoi(ex) : 1;
-    }
+    g.expand = o.two_hop < 0 ? 0 : 1;      // two hops per round through tasks and PUs
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
     const int sgrid = s.sparse_grid();     // sparse Bellman-Ford rounds
     const int wgrid = s.sweep_grid();      // sweeps
     const int ngrid = grid_for(nn, 2048);
-    const int alpha = s.opts.alpha >= 2 ? s.opts.alpha : 16;
-    int gi_base = s.opts.gu_interval > 0 ? s.opts.gu_interval : 8;
+    const int alpha = o.alpha >= 2 ? o.alpha : 8;
+    int gi_base = o.gu_interval > 0 ? o.gu_interval : 24;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
-    int pr_cap = 160;                              // price-refinement rounds before giving up (KS_PR_CAP)
-    if (const char* pc = std::getenv("KS_PR_CAP")) pr_cap = std::max(1, std::atoi(pc));
-    const bool use_pr = s.opts.price_refine != 0;
+    const int pr_cap = o.pr_rounds > 0 ? o.pr_rounds : 160;  // price-refinement rounds before giving up
+    const bool use_pr = o.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
-    if (const char* pd = std::getenv("KS_PR_DIV")) pr_div = std::max(1LL, std::atoll(pd));
-    const bool cycle_log = std::getenv("KS_CYCLE_LOG") != nullptr;
+    const bool cycle_log = o.log_cycles != 0;
     const int nhit = s.nhitems;
-    bool use_aug = true;   // tail augmentation (KS_AUG=0 disables it)
-    if (const char* ea = std::getenv("KS_AUG")) use_aug = std::atoi(ea) != 0;
-    int aug_slack = 4;     // walks take arcs of reduced cost <= aug_slack·ε (KS_AUG_SLACK)
-    if (const char* es = std::getenv("KS_AUG_SLACK")) aug_slack = std::max(1, std::atoi(es));
+    const bool use_aug = o.walk_slack >= 0;               // tail augmentation (walks)
+    const int aug_slack = o.walk_slack > 0 ? o.walk_slack : 4;   // walks take arcs of rc <= slack·ε
     // Bellman-Ford rounds enqueued per cycle: the last update's count + kb_margin,
     // at least kb_min (a launch that finds the update converged still costs ≈ 5 µs
     // with the gap before the next kernel; an update that needs more than was
     // enqueued costs a whole extra cycle)
-    int kb_margin = 6, kb_min = 8;
-    if (const char* km = std::getenv("KS_KB_MARGIN")) kb_margin = std::max(0, std::atoi(km));
-    if (const char* kn = std::getenv("KS_KB_MIN")) kb_min = std::max(1, std::atoi(kn));
+    const int kb_margin = o.bf_margin > 0 ? o.bf_margin : 6, kb_min = 8;
     bool pr_failed = false;   // the last phase's refinement did not certify the flow
-    bool pr_fail_thr = true;  // KS_PRFAIL_THR=0: the next phase saturates every negative arc
-    if (const char* pf = std::getenv("KS_PRFAIL_THR")) pr_fail_thr = std::atoi(pf) != 0;
-    int gi_tail = 4;       // sweeps per cycle once at most AUG_K nodes hold excess (even)
-    if (const char* et = std::getenv("KS_TAIL_GI")) gi_tail = std::max(2, std::min(MAXB, std::atoi(et))) & ~1;   // diagnostic: one stderr line per cycle
+    const int gi_tail = o.tail_sweeps > 0 ? std::max(2, std::min(MAXB, (int)o.tail_sweeps)) & ~1 : 4;
     // A phase that another phase follows may end with a few excess nodes left:
     // refine's start (saturate every negative reduced cost) accepts any
     // pseudoflow, so the next, finer phase absorbs them with its own excess.
@@ -3552,20 +3553,17 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // end with a feasible flow. A coarse phase ends once at most phase_exit
     // nodes AND at most 1/phase_frac of its peak hold excess (the relative bound
     // keeps phases that start small — incremental rounds — doing their share).
-    // phase_exit = 0 disables the early end.
-    int phase_exit = 256, phase_frac = 128;
-    if (const char* pe = std::getenv("KS_PHASE_EXIT")) phase_exit = std::max(0, std::atoi(pe));
-    if (const char* pf = std::getenv("KS_PHASE_FRAC")) phase_frac = std::max(1, std::atoi(pf));
+    const int phase_exit = o.phase_exit < 0 ? 0 : (o.phase_exit > 0 ? o.phase_exit : 256);
+    const int phase_frac = o.phase_frac > 0 ? o.phase_frac : 128;
     // ε schedule: the phase that price refinement certifies runs at 1/D of a cost
-    // unit (D = 48; KS_FINAL_DIV), the others at α-multiples of it, the first in
+    // unit (D = 48; ks_opts.final_div), the others at α-multiples of it, the first in
     // [max|cost|/α², max|cost|/α) scaled. Measured on config 3 (40 solves each):
     // ending at 1/32 of a unit (the plain max|cost|/α^k sequence) left the flow
     // short of optimal in 15 of 40 solves — a sixth phase, ≈ 28 ms — at 1/48 in
     // none; 1/64 and 1/96 cost more per phase.
     long long eps = std::max<long long>(1, maxc * mult);
     {
-        long long D = 48;
-        if (const char* fd = std::getenv("KS_FINAL_DIV")) D = std::max(0LL, std::atoll(fd));
+        const long long D = o.final_div < 0 ? 0 : (o.final_div > 0 ? o.final_div : 48);
         if (D > 0 && use_pr && maxc > 0) {
             long long e = std::max<long long>(1, (mult - 1) / D);
             const long long lo = std::max<long long>(1, eps / ((long long)alpha * alpha));
@@ -3628,48 +3626,27 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         return ok;
     };
 
-    // warm start: the previous flow and prices (in place), fresh nodes priced off
-    // their out-arcs, then a start at a small ε (≤ K cost units, K = KS_WARM_K,
-    // default 8) saturating only the arcs that violate it
-    long long warm_thr = 0;
-    if (use_warm) {
-        hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
-                           (const unsigned char*)s.n_fresh.p, (const int*)s.perm.p, g);
-        if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
-        KS_CHECK(read_ctl());
-        long long K = 8;
-        long long D = 1;   // KS_WARM_D: start below one cost unit (K·mult / D)
-        if (const char* wk = std::getenv("KS_WARM_K")) K = std::max(1LL, std::atoll(wk));
-        if (const char* wd = std::getenv("KS_WARM_D")) D = std::max(1LL, std::atoll(wd));
-        const long long viol = s.h_ctl->gu_L;
-        const long long e0 = std::max<long long>(1, std::min<long long>({viol, K * mult / D, eps}));
-        warm_thr = e0;
-        eps = e0 * alpha;   // the first phase runs at e0
-        KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
-    }
-
-    do {
-        eps = std::max<long long>(1, eps / alpha);
-        ++phases;
-        KS_CHECK(set_eps(eps));
+    // One ε-phase from the pseudoflow in place: saturate every residual arc whose
+    // reduced cost is below −sat_thr (thr 0: Goldberg's refine start; thr ε: only
+    // the arcs that violate ε-optimality), then update/sweep cycles until no node
+    // holds excess — a coarse phase (may_end_early) may stop with a few excess
+    // nodes left for the next, finer one. walk_sl: the tail walks' slack (1 when the
+    // phase must end ε-optimal at ε = 1). Returns KS_OK, KS_E_INFEASIBLE (status),
+    // or a device / convergence error.
+    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl) -> int {
+        KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        // After a failed refinement the flow is feasible and ε-optimal at the old ε:
-        // saturating only the arcs that violate the new ε (rc < −ε) is a valid start
-        // (push-relabel at ε needs an ε-optimal pseudoflow, not a 0-optimal one) and
-        // disturbs far less than saturating every negative arc.
-        const long long sat_thr = phases == 1 && use_warm ? warm_thr : (pr_failed && pr_fail_thr ? eps : 0LL);
-        pr_failed = false;
         hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, sat_thr);
         KS_CHECK(hipEventRecord(s.ev[3], st));
         uint64_t phase_sweeps = 0;
         int gi = gi_base;     // sweeps in the next cycle (fewer in a phase's tail, where walks augment)
         int phase_peak = 0;   // most excess nodes seen by an update of this phase
+        int rc = KS_OK;
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
-        // [apply][gi sweeps][end: control block → pinned host memory].
+        // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
             hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
-            for (int r = 0; r < kb; ++r) {   // the first round may be the update's dense one
-                // sparse from the first round: k_gu_init flags the deficits
+            for (int r = 0; r < kb; ++r) {   // sparse from the first round: k_gu_init flags the deficits
                 hipLaunchKernelGGL(k_bf_round<false>, dim3(sgrid), dim3(BLK), 0, st, g, bseq, 0);
                 ++bseq;
                 ++bf_launches;
@@ -3680,12 +3657,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             if (use_aug) {   // tail augmentation: walkers, hub distribution, walkers from what it fed
-                // slack > 1 only while a finer phase or price refinement still follows (ε > 1):
-                // a phase at ε = 1 must end 1-optimal
-                const int sl = eps > 1 ? aug_slack : 1;
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, sl);
-                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, sl);
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, sl);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
+                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, walk_sl);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, walk_sl);
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
@@ -3710,7 +3684,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             ms_sw_k += t_sw;   // sweeps + cycle end
             prev_end = s.cdone[cur];
             if (hc->infeasible) {
-                status = KS_E_INFEASIBLE;
+                rc = KS_E_INFEASIBLE;
                 std::memcpy(s.h_ctl, hc, sizeof(Ctl));
                 break;
             }
@@ -3722,7 +3696,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             if (cycle_log) {
                 std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d n_exc %d walks %d/%d",
-                             phases, eps, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc,
+                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc,
                              hc->aug_reached, hc->aug_short);
                 for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
                     const int x = hc->dbg_x[k];
@@ -3744,9 +3718,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
             }
-            const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
             phase_peak = std::max(phase_peak, hc->n_exc);
-            if (!last_phase && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
+            if (may_end_early && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
@@ -3763,14 +3736,52 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipEventSynchronize(s.ev[5]));
         ms_sat += ev_ms(s.ev[2], s.ev[3]);
         ms_cycles += ev_ms(s.ev[3], s.ev[5]);
-        if (status) break;
+        return rc;
+    };
+
+    // warm start: the previous flow and prices (in place), fresh nodes priced off
+    // their out-arcs, then a start at a small ε (≤ 8 cost units) saturating only
+    // the arcs that violate it
+    long long warm_thr = 0;
+    if (use_warm) {
+        hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
+                           (const unsigned char*)s.n_fresh.p, (const int*)s.perm.p, g);
+        if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
+        KS_CHECK(read_ctl());
+        const long long viol = s.h_ctl->gu_L;
+        const long long e0 = std::max<long long>(1, std::min<long long>({viol, 8 * mult, eps}));
+        warm_thr = e0;
+        eps = e0 * alpha;   // the first phase runs at e0
+        KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
+    }
+
+    do {
+        eps = std::max<long long>(1, eps / alpha);
+        ++phases;
+        // After a failed refinement the flow is feasible and ε-optimal at the old ε:
+        // saturating only the arcs that violate the new ε (rc < −ε) is a valid start
+        // (push-relabel at ε needs an ε-optimal pseudoflow, not a 0-optimal one) and
+        // disturbs far less than saturating every negative arc.
+        const long long sat_thr = phases == 1 && use_warm ? warm_thr : (pr_failed ? eps : 0LL);
+        pr_failed = false;
+        const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
+        // walk slack > 1 only while a finer phase or price refinement still follows
+        // (ε > 1): a phase at ε = 1 must end 1-optimal (fault_inject bit 0 breaks
+        // exactly this, for the certificate-recovery test)
+        const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
+        const int rc = run_phase(eps, sat_thr, !last_phase, walk_sl);
+        if (rc == KS_E_INFEASIBLE) {
+            status = rc;
+            break;
+        }
+        if (rc) return rc;
         // certify optimality early: a flow that is 1-optimal (scaled) is optimal.
         // Tried once ε is below 1/32 of a cost unit, where it usually succeeds.
         if (use_pr && eps > 1 && eps * pr_div < mult) {
             int used = 0;
-            int rc = price_refine(1, &used, pr_cap);
-            if (rc < 0) return rc;
-            if (rc == 1) eps = 1;
+            const int pr = price_refine(1, &used, pr_cap);
+            if (pr < 0) return pr;
+            if (pr == 1) eps = 1;
             else pr_failed = true;
         }
     } while (eps > 1);
@@ -3784,10 +3795,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
               std::to_string(gus) + ", sweeps " + std::to_string(sweep_launches) + ")";
 
     // ------------------------------------------------------------ verify ---
-    KS_CHECK(hipEventRecord(s.ev[6], st));
+    // Conservation, capacity, 1-optimality of the final prices (scaled units), the
+    // int64 cost and the flow value measured from the resident flow. → verify_bad bits
     const int vgrid = grid_for(hi, 2048);
     long long tot_cost = 0, tot_flow = 0;
-    if (status == KS_OK) {
+    auto verify = [&](int* bad) -> int {
+        KS_CHECK(hipMemsetAsync(&s.ctl.p->verify_bad, 0, sizeof(int), st));
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
         if (hi)
@@ -3805,13 +3818,46 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                     st));
         }
         KS_CHECK(read_ctl());
+        tot_cost = tot_flow = 0;
         for (long long x : parts) tot_cost += x;
         for (long long x : partf) tot_flow += x;
-        if (s.h_ctl->verify_bad && s.opts.verify) {
+        *bad = s.h_ctl->verify_bad;
+        return KS_OK;
+    };
+    KS_CHECK(hipEventRecord(s.ev[6], st));
+    if (status == KS_OK) {
+        if (o.fault_inject & 2)   // TESTS ONLY: break the certificate, not the flow
+            hipLaunchKernelGGL(k_perturb_price, dim3(1), dim3(1), 0, st, g, 0, 1000 * mult);
+        int bad = 0;
+        int rc = verify(&bad);
+        if (rc) return rc;
+        // A failed optimality certificate on a feasible flow is repaired, not fatal:
+        // price refinement at ε = 1 (the flow may be optimal, only its prices off),
+        // else one more ε = 1 phase from the current flow (saturating only the arcs
+        // that violate 1-optimality), then verification again. Capacity and
+        // conservation violations stay fatal (KS_E_VERIFY).
+        for (int attempt = 0; attempt < 2 && bad == 2; ++attempt) {
+            ++res.recoveries;
+            int used = 0;
+            const int pr = price_refine(1, &used, 4 * pr_cap);
+            if (pr < 0) return pr;
+            if (pr == 0) {
+                ++phases;
+                rc = run_phase(1, 1, false, 1);
+                if (rc == KS_E_INFEASIBLE) {
+                    status = rc;
+                    err = "infeasible during certificate recovery";
+                    break;
+                }
+                if (rc) return rc;
+            }
+            rc = verify(&bad);
+            if (rc) return rc;
+        }
+        if (status == KS_OK && bad && o.verify) {
             status = KS_E_VERIFY;
-            err = std::string("on-device verification failed (") +
-                  ((s.h_ctl->verify_bad & 1) ? "capacity " : "") + ((s.h_ctl->verify_bad & 2) ? "optimality " : "") +
-                  ((s.h_ctl->verify_bad & 4) ? "conservation" : "") + ")";
+            err = std::string("on-device verification failed (") + ((bad & 1) ? "capacity " : "") +
+                  ((bad & 2) ? "optimality " : "") + ((bad & 4) ? "conservation" : "") + ")";
         }
     }
     KS_CHECK(hipEventRecord(s.ev[7], st));
@@ -3822,7 +3868,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
     if (cycle_log)
-        std::fprintf(stderr, "solve tail walks to a deficit %llu, hops %llu\n", tc[C_AUGWALK], tc[C_AUGHOP]);
+        std::fprintf(stderr, "solve tail walks to a deficit %llu, hops %llu, recoveries %d\n", tc[C_AUGWALK],
+                     tc[C_AUGHOP], res.recoveries);
 
 #ifdef KS_STAMPS
     if (stamp_path && s.stamps.n > 1) {

@@ -137,9 +137,12 @@ void account(ks_ctx* c, uint64_t id, const NodeRec& r, int sign) {
     if (r.type == KS_NODE_TASK) c->n_tasks += sign;
 }
 
-int check_arc(ks_ctx* c, uint64_t s, uint64_t d, uint64_t low, uint64_t cap, int64_t cost) {
+// Validate one arc against a node table (the context's, or a load's new one).
+int check_arc(ks_ctx* c, const std::vector<NodeRec>& tab, uint64_t s, uint64_t d, uint64_t low, uint64_t cap,
+              int64_t cost) {
+    auto alive = [&](uint64_t id) { return id < tab.size() && tab[id].alive; };
     if (s == 0 || d == 0 || s >= kMaxId || d >= kMaxId) return c->fail(KS_E_RANGE, "arc endpoint id out of range");
-    if (!node_alive(c, s) || !node_alive(c, d))
+    if (!alive(s) || !alive(d))
         return c->fail(KS_E_INVALID, "arc " + std::to_string(s) + "->" + std::to_string(d) + " has a missing endpoint");
     if (s == d) return c->fail(KS_E_INVALID, "self-loop arc at node " + std::to_string(s));
     if (low > (uint64_t)INT64_MAX || cap > (uint64_t)INT64_MAX) return c->fail(KS_E_RANGE, "arc bound exceeds int64");
@@ -148,6 +151,17 @@ int check_arc(ks_ctx* c, uint64_t s, uint64_t d, uint64_t low, uint64_t cap, int
     if (cap > (uint64_t(1) << 53) || cost > (int64_t(1) << 40) || cost < -(int64_t(1) << 40))
         return c->fail(KS_E_RANGE, "arc capacity or cost outside the supported range");
     return KS_OK;
+}
+int check_arc(ks_ctx* c, uint64_t s, uint64_t d, uint64_t low, uint64_t cap, int64_t cost) {
+    return check_arc(c, c->nodes, s, d, low, cap, cost);
+}
+
+// A device-side failure inside an apply or a load leaves the device store in an
+// unknown state: every call that would read it refuses until the next load.
+int store_guard(ks_ctx* c) {
+    if (!c->store_bad) return KS_OK;
+    return c->fail(KS_E_INVALID, "the device graph store is inconsistent after a failed load or apply: "
+                                 "reload the graph (ks_load_graph)");
 }
 
 }  // namespace
@@ -203,6 +217,13 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
             return c->fail(KS_E_INVALID, "node " + std::to_string(nodes[i].id) + " already present");
         r = NodeRec{nodes[i].excess, nodes[i].type, true, true};
     }
+    // every arc is checked against the new table BEFORE anything changes: a bad
+    // arc leaves the context (host and device) exactly as it was
+    for (size_t i = 0; i < m; ++i) {
+        const ks_arc& a = arcs[i];
+        int rc = check_arc(c, fresh, a.src, a.dst, a.low, a.cap, a.cost);
+        if (rc) return rc;
+    }
     c->nodes.swap(fresh);
     c->epoch_of.assign(maxid + 1, 0);
     c->lastrm_of.assign(maxid + 1, -1);
@@ -211,15 +232,6 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     for (uint64_t id = 1; id <= maxid; ++id) account(c, id, c->nodes[id], 1);
     c->have_solution = false;
     c->flows_fresh = false;
-    for (size_t i = 0; i < m; ++i) {
-        const ks_arc& a = arcs[i];
-        int rc = check_arc(c, a.src, a.dst, a.low, a.cap, a.cost);
-        if (rc) {
-            c->nodes.assign(1, NodeRec{});   // no half-loaded graph
-            c->sum_others = c->n_sinks = c->n_tasks = 0;
-            return rc;
-        }
-    }
     std::vector<int64_t> supply(maxid);
     std::vector<uint8_t> type(maxid), alive(maxid);
     for (uint64_t id = 1; id <= maxid; ++id) {
@@ -229,7 +241,9 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
         alive[id - 1] = r.alive ? 1 : 0;
     }
     c->dev_sink_supply = (c->n_sinks == 1) ? c->nodes[c->sink_id].excess : 0;
-    return c->eng.load((int64_t)maxid, supply.data(), type.data(), alive.data(), arcs, m, c->err);
+    const int rc = c->eng.load((int64_t)maxid, supply.data(), type.data(), alive.data(), arcs, m, c->err);
+    c->store_bad = rc != KS_OK;   // the upload failed part-way: nothing may read the store
+    return rc;
 }
 
 // Validate the stream in order against node liveness (graph.go / the change
@@ -239,6 +253,7 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     if (!c) return KS_E_INVALID;
     if (k && !d) return c->fail(KS_E_INVALID, "null delta array");
     if (k > (size_t)INT32_MAX) return c->fail(KS_E_RANGE, "delta stream too long");
+    if (int g = store_guard(c)) return g;
     if (++c->epoch == 0) {   // epoch wrapped: forget old stamps
         std::fill(c->epoch_of.begin(), c->epoch_of.end(), 0);
         c->epoch = 1;
@@ -308,6 +323,8 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     }
     std::vector<ks::NodeEdit> edits;
     edits.reserve(saved.size());
+    const int64_t sum0 = c->sum_others, sinks0 = c->n_sinks, tasks0 = c->n_tasks, dsink0 = c->dev_sink_supply;
+    const uint64_t sink0 = c->sink_id;
     for (const auto& sv : saved) {
         const uint64_t id = sv.first;
         const NodeRec& now = c->nodes[id];
@@ -326,7 +343,20 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     }
     c->have_solution = false;
     c->flows_fresh = false;
-    return c->eng.apply(edits.data(), edits.size(), d, k, c->nslots(), c->err);
+    rc = c->eng.apply(edits.data(), edits.size(), d, k, c->nslots(), c->err);
+    if (rc) {
+        // the device may have applied part of the stream: the host goes back to its
+        // state before the call (nodes and aggregates) and the store is marked
+        // unusable until the next ks_load_graph
+        for (auto it = saved.rbegin(); it != saved.rend(); ++it) c->nodes[it->first] = it->second;
+        c->sum_others = sum0;
+        c->n_sinks = sinks0;
+        c->n_tasks = tasks0;
+        c->sink_id = sink0;
+        c->dev_sink_supply = dsink0;
+        c->store_bad = true;
+    }
+    return rc;
 }
 
 // Coalescing follows the store's semantics above: ADD_ARC and UPDATE_ARC are both
@@ -426,6 +456,13 @@ int ks_coalesce_deltas(const ks_delta* in, size_t k, ks_delta* out, size_t cap, 
 
 int ks_solve(ks_ctx* c, ks_result* out) {
     if (!c) return KS_E_INVALID;
+    if (int g = store_guard(c)) {
+        if (out) {
+            std::memset(out, 0, sizeof(*out));
+            out->status = g;
+        }
+        return g;
+    }
     ks_result r;
     std::memset(&r, 0, sizeof(r));
     c->have_solution = false;
@@ -523,6 +560,7 @@ int ks_get_task_pu_device(ks_ctx* c, uint64_t* dev_out, size_t cap, size_t* coun
 
 int ks_set_bindings(ks_ctx* c, const uint64_t* task, const uint64_t* pu, size_t k) {
     if (!c) return KS_E_INVALID;
+    if (int g = store_guard(c)) return g;
     if (k && (!task || !pu)) return c->fail(KS_E_INVALID, "null binding array");
     for (size_t i = 0; i < k; ++i) {
         if (!node_alive(c, task[i]) || c->nodes[task[i]].type != KS_NODE_TASK)
@@ -557,6 +595,7 @@ int ks_scheduling_deltas(ks_ctx* c, int commit, ks_sched_delta* out, size_t cap,
 int ks_update_unsched_costs(ks_ctx* c, const uint64_t* ids, size_t k, int32_t mode, int64_t unsched_cost,
                             int64_t continuation_cost, size_t* changed) {
     if (!c) return KS_E_INVALID;
+    if (int g = store_guard(c)) return g;
     if (mode != KS_COST_SET && mode != KS_COST_ADD) return c->fail(KS_E_INVALID, "unknown cost mode");
     const int64_t lim = int64_t(1) << 40;
     if (unsched_cost > lim || unsched_cost < -lim || continuation_cost > lim || continuation_cost < -lim)
@@ -577,6 +616,7 @@ int ks_update_unsched_costs(ks_ctx* c, const uint64_t* ids, size_t k, int32_t mo
 int ks_topology_stats(ks_ctx* c, uint64_t max_tasks_per_pu, const uint64_t* pu_ids, const uint64_t* pu_running,
                       size_t k, uint64_t* slots_below, uint64_t* running_below, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
+    if (int g = store_guard(c)) return g;
     const size_t n = (size_t)c->nslots();
     *count = n;
     if (!slots_below || !running_below) return KS_OK;
@@ -594,6 +634,7 @@ int ks_topology_stats(ks_ctx* c, uint64_t max_tasks_per_pu, const uint64_t* pu_i
 
 int ks_get_graph(ks_ctx* c, ks_node* nodes, size_t ncap, size_t* n, ks_arc* arcs, size_t acap, size_t* m) {
     if (!c || !n || !m) return KS_E_INVALID;
+    if (int g = store_guard(c)) return g;
     size_t k = 0;
     for (uint64_t id = 1; id < c->nodes.size(); ++id) {
         const NodeRec& r = c->nodes[id];

@@ -23,7 +23,9 @@ EXPORTED_SYMBOLS = (
     "ks_update_unsched_costs", "ks_topology_stats", "ks_get_graph",
     "ks_batch_create", "ks_batch_create_rank", "ks_batch_unique_id", "ks_batch_destroy", "ks_batch_last_error",
     "ks_batch_load", "ks_batch_solve", "ks_batch_gather",
+    "ks_batch_slots", "ks_batch_owner", "ks_batch_block_len", "ks_batch_unpack",
 )
+ABI_VERSION = 2
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
 
@@ -42,9 +44,13 @@ FLOW_DT = np.dtype({"names": ["src", "dst", "flow"], "formats": ["<u8", "<u8", "
 
 
 class KsOpts(C.Structure):
+    """ks_opts (include/ksmcmf.h): 0 in a tuning field selects the library default."""
     _fields_ = [("alpha", C.c_int32), ("verify", C.c_int32), ("auto_sink", C.c_int32),
                 ("price_refine", C.c_int32), ("gu_interval", C.c_int32), ("warm_start", C.c_int32),
-                ("reserved", C.c_int32 * 10)]
+                ("walk_slack", C.c_int32), ("final_div", C.c_int32), ("pr_rounds", C.c_int32),
+                ("phase_exit", C.c_int32), ("phase_frac", C.c_int32), ("tail_sweeps", C.c_int32),
+                ("bf_margin", C.c_int32), ("two_hop", C.c_int32), ("log_cycles", C.c_int32),
+                ("fault_inject", C.c_int32), ("reserved", C.c_int32 * 8)]
 
 
 class KsResult(C.Structure):
@@ -55,10 +61,10 @@ class KsResult(C.Structure):
                 ("ms_phase", C.c_double * 6), ("n_nodes", C.c_int64), ("n_arcs", C.c_int64),
                 ("sweep_launches", C.c_uint64), ("ms_sweep_kernels", C.c_double),
                 ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double), ("warm_started", C.c_int32),
-                ("rebuilt", C.c_int32)]
+                ("rebuilt", C.c_int32), ("recoveries", C.c_int32), ("_pad", C.c_int32)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ms_phase"}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "_pad")}
         names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d
@@ -137,6 +143,12 @@ def load(build_if_missing: bool = True):
     L.ks_batch_load.argtypes = [V, C.c_size_t, P(V), P(C.c_size_t), P(V), P(C.c_size_t)]
     L.ks_batch_solve.argtypes = [V, P(KsResult)]
     L.ks_batch_gather.argtypes = [V, C.c_size_t, V, V, V]
+    L.ks_batch_slots.argtypes = [C.c_size_t, C.c_int]
+    L.ks_batch_slots.restype = C.c_size_t
+    L.ks_batch_owner.argtypes = [C.c_size_t, C.c_int, P(C.c_int), P(C.c_size_t)]
+    L.ks_batch_block_len.argtypes = [C.c_size_t, C.c_int, C.c_size_t]
+    L.ks_batch_block_len.restype = C.c_size_t
+    L.ks_batch_unpack.argtypes = [V, C.c_size_t, C.c_int, C.c_size_t, V, V, V]
     L.ks_set_bindings.argtypes = [V, V, V, C.c_size_t]
     L.ks_scheduling_deltas.argtypes = [V, C.c_int, V, C.c_size_t, P(C.c_size_t)]
     L.ks_update_unsched_costs.argtypes = [V, V, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_size_t)]
@@ -386,6 +398,31 @@ class Batch:
         p = lambda a: None if a is None else a.ctypes.data
         self._check(self._L.ks_batch_gather(self._h, max_tasks, p(pu), p(cost), p(flow)))
         return pu, cost, flow
+
+
+def batch_owner(g: int, world: int) -> tuple[int, int]:
+    """ks_batch_owner: (global rank, slot on that rank) of graph g."""
+    r, sl = C.c_int(), C.c_size_t()
+    if load().ks_batch_owner(g, world, C.byref(r), C.byref(sl)) != KS_OK:
+        raise KsError(KS_E_INVALID, "ks_batch_owner")
+    return r.value, sl.value
+
+
+def batch_block_len(ngraphs: int, world: int, max_tasks: int) -> int:
+    return int(load().ks_batch_block_len(ngraphs, world, max_tasks))
+
+
+def batch_unpack(gathered: np.ndarray, ngraphs: int, world: int, max_tasks: int):
+    """ks_batch_unpack over the world blocks rank 0 received → (pu, cost, flow) in graph order."""
+    gathered = np.ascontiguousarray(gathered, np.int64)
+    pu = np.zeros((ngraphs, max_tasks), np.uint64)
+    cost = np.zeros(ngraphs, np.int64)
+    flow = np.zeros(ngraphs, np.int64)
+    rc = load().ks_batch_unpack(gathered.ctypes.data, ngraphs, world, max_tasks, pu.ctypes.data, cost.ctypes.data,
+                                flow.ctypes.data)
+    if rc != KS_OK:
+        raise KsError(rc, "ks_batch_unpack: a rank reported a failure")
+    return pu, cost, flow
 
 
 def solve_many(ctxs: list[Context], workers: int = 0) -> list[SolveResult]:

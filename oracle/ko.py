@@ -50,6 +50,16 @@ def lib():
         L.ko_flow_lines.restype = C.c_int64
         L.ko_bfs_mapping_from_lines.argtypes = [P(KoGraph), C.c_char_p, C.c_int64, P(C.c_int64), P(C.c_int64)]
         L.ko_bfs_mapping_from_lines.restype = C.c_int64
+        V = C.c_void_p
+        L.ko_ssp_incremental.argtypes = [P(KoGraph), V, V, V, C.c_int64, V, C.c_int64, V, V, V,
+                                         P(C.c_int64), P(C.c_int64), P(C.c_int64), P(C.c_double)]
+        L.ko_reference_path_incremental.argtypes = [P(KoGraph), V, C.c_int64, V, V, V, C.c_int64, V, C.c_int64, V,
+                                                    V, V, P(C.c_int64), P(C.c_int64), P(C.c_int64),
+                                                    P(C.c_double)]
+        L.ko_export_changes.argtypes = [V, C.c_int64, C.c_char_p, C.c_int64]
+        L.ko_export_changes.restype = C.c_int64
+        L.ko_parse_changes.argtypes = [C.c_char_p, C.c_int64, V, C.c_int64]
+        L.ko_parse_changes.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -141,6 +151,69 @@ def bfs_mapping_from_text(g, text: str):
     if k < 0:
         raise RuntimeError("Task Node to Resource Node should be 1:1 mapping")
     return dict(zip(tk[:k].tolist(), pu[:k].tolist()))
+
+
+DELTA_DT = np.dtype({"names": ["kind", "type", "id", "src", "dst", "low", "cap", "cost", "old_cost", "excess"],
+                     "formats": ["<i4", "<i4", "<u8", "<u8", "<u8", "<u8", "<u8", "<i8", "<i8", "<i8"],
+                     "offsets": [0, 4, 8, 16, 24, 32, 40, 48, 56, 64], "itemsize": 72})
+
+
+class IncrementalSSP:
+    """Flowlessly's daemon mode restated (ko_ssp_incremental): each round re-solves
+    from the previous round's flow (carried by (src, dst)) and potentials (by node
+    id). ``round(g, deltas, fresh_ids)`` runs the whole later-Solve reference path:
+    the change block as text and parsed back, the incremental SSP, the "f" lines
+    and the BFS mapping (ko_reference_path_incremental). The first call (no
+    previous state) is a cold SSP."""
+
+    def __init__(self):
+        self.src = self.dst = self.flow = self.pot = None
+        self.last = None
+
+    def round(self, g, deltas=None, fresh_ids=()):
+        h = _Holder(g)
+        n, m = h.ntype.shape[0], h.src.shape[0]
+        flow = np.zeros(m, np.int64)
+        pot = np.zeros(n, np.int64)
+        cost, fv, nm = C.c_int64(), C.c_int64(), C.c_int64()
+        ms = (C.c_double * 6)()
+        if self.pot is None:
+            self.src = np.zeros(0, np.int64)
+            self.dst = np.zeros(0, np.int64)
+            self.flow = np.zeros(0, np.int64)
+            self.pot = np.zeros(0, np.int64)
+        fresh = np.zeros(n, np.uint8)
+        ids = np.asarray(list(fresh_ids), np.int64)
+        if ids.size:
+            fresh[ids - 1] = 1
+        d = np.ascontiguousarray(deltas if deltas is not None else np.zeros(0, DELTA_DT), DELTA_DT)
+        cp = lambda a: a.ctypes.data
+        st = lib().ko_reference_path_incremental(
+            C.byref(h.kg), cp(d), d.shape[0], cp(self.src), cp(self.dst), cp(self.flow), self.src.shape[0],
+            cp(self.pot), self.pot.shape[0], cp(fresh), cp(flow), cp(pot), C.byref(cost), C.byref(fv),
+            C.byref(nm), ms)
+        if st < 0:
+            raise RuntimeError(f"ko_reference_path_incremental failed ({st})")
+        self.src, self.dst, self.flow, self.pot = h.src.copy(), h.dst.copy(), flow, pot
+        self.last = {"status": st, "cost": cost.value, "flow": fv.value, "mapped": nm.value,
+                     "ms": dict(zip(("export", "parse", "carry", "saturate", "augment", "flines_bfs"), list(ms)))}
+        return st, cost.value, fv.value, flow
+
+    def export_changes(self, deltas) -> str:
+        d = np.ascontiguousarray(deltas, DELTA_DT)
+        need = lib().ko_export_changes(d.ctypes.data, d.shape[0], None, 0)
+        buf = C.create_string_buffer(int(need) + 1)
+        ln = lib().ko_export_changes(d.ctypes.data, d.shape[0], buf, need + 1)
+        return buf.raw[:ln].decode()
+
+
+def parse_changes(text: str) -> np.ndarray:
+    raw = text.encode()
+    out = np.zeros(raw.count(b"\n") + 1, DELTA_DT)
+    k = lib().ko_parse_changes(raw, len(raw), out.ctypes.data, out.shape[0])
+    if k < 0:
+        raise ValueError("malformed change block")
+    return out[:k]
 
 
 def gen_quincy(T, M, R, J, seed):

@@ -250,48 +250,19 @@ static void hp_pop(heap_t* h, int64_t* key, int64_t* val) {
 /* successive shortest path (Flowlessly's configured algorithm, solver.go:32)  */
 /* reduced cost rc(u,v) = c + pot[u] − pot[v] ≥ 0 on residual arcs            */
 /* ------------------------------------------------------------------------- */
-int ko_ssp(const ko_graph* g, int64_t* flow_out, int64_t* total_cost, int64_t* flow_value,
-           int64_t* augmentations) {
-    res_t r;
-    if (res_build(g, &r)) return -1;
+
+/* Augment every excess node's supply along shortest paths (Dijkstra with the
+ * potentials, stopped at the first deficit settled). Requires rc ≥ 0 on every
+ * residual arc; keeps it (pot[v] += dist[v] − D for settled v). Returns the
+ * number of augmentations. */
+static int64_t ssp_augment_all(res_t* rp, int64_t* pot) {
+    res_t r = *rp;
     const int64_t n = r.n;
-    int64_t* pot = (int64_t*)calloc(n + 1, sizeof(int64_t));
     int64_t* dist = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
     int64_t* pred = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
     char* done = (char*)calloc(n + 1, 1);
     int64_t* touched = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
     for (int64_t v = 0; v < n; ++v) dist[v] = KO_INF;
-
-    /* initial potentials: Bellman-Ford (SPFA) when a residual arc has negative cost */
-    int neg = 0;
-    for (int64_t a = 0; a < 2 * r.m; ++a) if (r.rcap[a] > 0 && r.cost[a] < 0) { neg = 1; break; }
-    if (neg) {
-        int64_t* q = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
-        char* inq = (char*)malloc(n + 1);
-        int64_t* cnt = (int64_t*)calloc(n + 1, sizeof(int64_t));
-        int64_t qh = 0, qt = 0, qn = 0;
-        for (int64_t v = 0; v < n; ++v) { pot[v] = 0; q[qt++] = v; inq[v] = 1; ++qn; }
-        if (qt == n + 1) qt = 0;
-        while (qn > 0) {
-            const int64_t u = q[qh++]; if (qh == n + 1) qh = 0; --qn; inq[u] = 0;
-            for (int64_t a = r.first[u]; a < r.first[u + 1]; ++a) {
-                if (r.rcap[a] <= 0) continue;
-                const int64_t v = r.head[a];
-                if (pot[u] + r.cost[a] < pot[v]) {
-                    pot[v] = pot[u] + r.cost[a];
-                    if (!inq[v]) {
-                        if (++cnt[v] > n + 1) { /* negative cycle */
-                            free(q); free(inq); free(cnt); free(pot); free(dist); free(pred);
-                            free(done); free(touched); res_free(&r); return -3;
-                        }
-                        q[qt++] = v; if (qt == n + 1) qt = 0; ++qn; inq[v] = 1;
-                    }
-                }
-            }
-        }
-        free(q); free(inq); free(cnt);
-    }
-
     heap_t h;
     hp_init(&h, 1024);
     int64_t naug = 0;
@@ -350,6 +321,47 @@ int ko_ssp(const ko_graph* g, int64_t* flow_out, int64_t* total_cost, int64_t* f
         }
     }
     hp_free(&h);
+    free(dist); free(pred); free(done); free(touched);
+    return naug;
+}
+
+int ko_ssp(const ko_graph* g, int64_t* flow_out, int64_t* total_cost, int64_t* flow_value,
+           int64_t* augmentations) {
+    res_t r;
+    if (res_build(g, &r)) return -1;
+    const int64_t n = r.n;
+    int64_t* pot = (int64_t*)calloc(n + 1, sizeof(int64_t));
+
+    /* initial potentials: Bellman-Ford (SPFA) when a residual arc has negative cost */
+    int neg = 0;
+    for (int64_t a = 0; a < 2 * r.m; ++a) if (r.rcap[a] > 0 && r.cost[a] < 0) { neg = 1; break; }
+    if (neg) {
+        int64_t* q = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
+        char* inq = (char*)malloc(n + 1);
+        int64_t* cnt = (int64_t*)calloc(n + 1, sizeof(int64_t));
+        int64_t qh = 0, qt = 0, qn = 0;
+        for (int64_t v = 0; v < n; ++v) { pot[v] = 0; q[qt++] = v; inq[v] = 1; ++qn; }
+        if (qt == n + 1) qt = 0;
+        while (qn > 0) {
+            const int64_t u = q[qh++]; if (qh == n + 1) qh = 0; --qn; inq[u] = 0;
+            for (int64_t a = r.first[u]; a < r.first[u + 1]; ++a) {
+                if (r.rcap[a] <= 0) continue;
+                const int64_t v = r.head[a];
+                if (pot[u] + r.cost[a] < pot[v]) {
+                    pot[v] = pot[u] + r.cost[a];
+                    if (!inq[v]) {
+                        if (++cnt[v] > n + 1) { /* negative cycle */
+                            free(q); free(inq); free(cnt); free(pot); res_free(&r); return -3;
+                        }
+                        q[qt++] = v; if (qt == n + 1) qt = 0; ++qn; inq[v] = 1;
+                    }
+                }
+            }
+        }
+        free(q); free(inq); free(cnt);
+    }
+
+    const int64_t naug = ssp_augment_all(&r, pot);
 
     int64_t left = 0;
     for (int64_t v = 0; v < n; ++v) if (r.excess[v] > 0) left += r.excess[v];
@@ -359,7 +371,108 @@ int ko_ssp(const ko_graph* g, int64_t* flow_out, int64_t* total_cost, int64_t* f
     *total_cost = c;
     *flow_value = r.pos_supply - left;
     if (augmentations) *augmentations = naug;
-    free(pot); free(dist); free(pred); free(done); free(touched);
+    free(pot);
+    res_free(&r);
+    return left > 0 ? 1 : 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* incremental SSP: the daemon mode ksched runs Flowlessly in                   */
+/* (solver.go:30-34 Incremental = true; later Solves send only the change     */
+/* block, :86-89, and the solver re-solves from its previous state)            */
+/* ------------------------------------------------------------------------- */
+static inline uint64_t arc_key64(int64_t s, int64_t d) { return ((uint64_t)s << 32) | (uint64_t)d; }
+static inline uint64_t key_hash(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33;
+    return k;
+}
+
+/* The previous round's flow is carried by (src, dst) key onto the new graph
+ * (clamped to the new bounds: a lowered capacity returns its surplus to the
+ * endpoints, a deleted arc's flow leaves its endpoints unbalanced, a removed
+ * node's arcs are gone), the previous potentials by node id (nodes created since
+ * — fresh[v] = 1 — get the least potential under which none of their residual
+ * out-arcs is negative). Every residual arc that the changes left with negative
+ * reduced cost is then saturated, which restores rc ≥ 0 everywhere at the price
+ * of more excess and deficit, and successive shortest paths route every excess
+ * to a deficit from there. flow_out / pot_out: m / n entries for the next round.
+ * ms[0] carry (hash the old arcs, seed the residual graph), ms[1] saturate,
+ * ms[2] augment. */
+int ko_ssp_incremental(const ko_graph* g, const int64_t* prev_src, const int64_t* prev_dst,
+                       const int64_t* prev_flow, int64_t prev_m, const int64_t* prev_pot, int64_t prev_n,
+                       const uint8_t* fresh, int64_t* flow_out, int64_t* pot_out, int64_t* total_cost,
+                       int64_t* flow_value, int64_t* augmentations, double* ms) {
+    const double t0 = now_ms();
+    res_t r;
+    if (res_build(g, &r)) return -1;
+    const int64_t n = r.n, m = r.m;
+    /* (src, dst) → previous flow */
+    int64_t hcap = 16;
+    while (hcap < 2 * prev_m + 2) hcap <<= 1;
+    uint64_t* hk = (uint64_t*)calloc(hcap, sizeof(uint64_t));
+    int64_t* hv = (int64_t*)malloc(sizeof(int64_t) * hcap);
+    for (int64_t i = 0; i < prev_m; ++i) {
+        if (prev_flow[i] <= 0) continue;
+        const uint64_t k = arc_key64(prev_src[i], prev_dst[i]);
+        uint64_t s = key_hash(k) & (uint64_t)(hcap - 1);
+        while (hk[s] && hk[s] != k) s = (s + 1) & (uint64_t)(hcap - 1);
+        hk[s] = k;
+        hv[s] = prev_flow[i];
+    }
+    for (int64_t i = 0; i < m; ++i) {
+        const uint64_t k = arc_key64(g->src[i], g->dst[i]);
+        uint64_t s = key_hash(k) & (uint64_t)(hcap - 1);
+        int64_t f = 0;
+        while (hk[s]) {
+            if (hk[s] == k) { f = hv[s]; break; }
+            s = (s + 1) & (uint64_t)(hcap - 1);
+        }
+        if (f < g->low[i]) f = g->low[i];
+        if (f > g->cap[i]) f = g->cap[i];
+        const int64_t x = f - g->low[i];   /* residual-graph flow (lower bounds transformed) */
+        if (x > 0) {
+            const int64_t p = r.fwd[i];
+            r.rcap[p] -= x;
+            r.rcap[r.rev[p]] += x;
+            r.excess[g->src[i] - 1] -= x;
+            r.excess[g->dst[i] - 1] += x;
+        }
+    }
+    free(hk); free(hv);
+    int64_t* pot = (int64_t*)calloc(n + 1, sizeof(int64_t));
+    for (int64_t v = 0; v < n && v < prev_n; ++v) pot[v] = prev_pot[v];
+    for (int64_t v = 0; v < n; ++v) {
+        if (v < prev_n && !(fresh && fresh[v])) continue;
+        int64_t best = INT64_MIN;   /* rc(v, w) = c + pot[v] − pot[w] ≥ 0 ⇔ pot[v] ≥ pot[w] − c */
+        for (int64_t a = r.first[v]; a < r.first[v + 1]; ++a)
+            if (r.rcap[a] > 0 && pot[r.head[a]] - r.cost[a] > best) best = pot[r.head[a]] - r.cost[a];
+        pot[v] = best == INT64_MIN ? 0 : best;
+    }
+    const double t1 = now_ms();
+    for (int64_t u = 0; u < n; ++u)
+        for (int64_t a = r.first[u]; a < r.first[u + 1]; ++a) {
+            if (r.rcap[a] <= 0) continue;
+            const int64_t v = r.head[a];
+            if (r.cost[a] + pot[u] - pot[v] < 0) {
+                const int64_t d = r.rcap[a];
+                r.rcap[a] = 0; r.rcap[r.rev[a]] += d;
+                r.excess[u] -= d; r.excess[v] += d;
+            }
+        }
+    const double t2 = now_ms();
+    const int64_t naug = ssp_augment_all(&r, pot);
+    const double t3 = now_ms();
+    int64_t left = 0;
+    for (int64_t v = 0; v < n; ++v) if (r.excess[v] > 0) left += r.excess[v];
+    res_flows(g, &r, flow_out);
+    int64_t c = 0;
+    for (int64_t i = 0; i < g->m; ++i) c += flow_out[i] * g->cost[i];
+    *total_cost = c;
+    *flow_value = r.pos_supply - left;
+    if (augmentations) *augmentations = naug;
+    if (pot_out) memcpy(pot_out, pot, sizeof(int64_t) * n);
+    if (ms) { ms[0] = t1 - t0; ms[1] = t2 - t1; ms[2] = t3 - t2; }
+    free(pot);
     res_free(&r);
     return left > 0 ? 1 : 0;
 }
@@ -770,6 +883,128 @@ int64_t ko_bfs_mapping_from_lines(const ko_graph* g, const char* lines, int64_t 
     for (int64_t v = 0; v < n; ++v) free(pus[v].a);
     free(pus); free(visited); free(queue); free(ifirst); free(isrc); free(iflow);
     return rc < 0 ? rc : nmap;
+}
+
+/* ExportIncremental (dimacs/export.go:31-38): one GenerateChange line per record
+ * (add_node_change.go:57-61 "n id excess type", create_arc_change.go:44-51
+ * "a src dst low cap cost type", update_arc_change.go:46-54
+ * "x src dst low cap cost type oldcost", remove_node_change.go:26-28 "r id"),
+ * then "c EOI". SET_EXCESS has no line (the reference never sends the sink's
+ * drift). Returns bytes written or the required size when buf is NULL. */
+int64_t ko_export_changes(const ko_delta* d, int64_t k, char* buf, int64_t cap) {
+    const int64_t need = 16 + k * (4 + 8 * 24);
+    if (!buf) return need;
+    if (cap < need) return -1;
+    char* p = buf;
+    for (int64_t i = 0; i < k; ++i) {
+        const ko_delta* x = &d[i];
+        switch (x->kind) {
+            case 0:
+                p = put_s(p, "n "); p = put_i64(p, (int64_t)x->id); *p++ = ' ';
+                p = put_i64(p, x->excess); *p++ = ' '; p = put_i64(p, x->type); *p++ = '\n';
+                break;
+            case 1:
+                p = put_s(p, "r "); p = put_i64(p, (int64_t)x->id); *p++ = '\n';
+                break;
+            case 2: case 3:
+                p = put_s(p, x->kind == 2 ? "a " : "x ");
+                p = put_i64(p, (int64_t)x->src); *p++ = ' '; p = put_i64(p, (int64_t)x->dst); *p++ = ' ';
+                p = put_i64(p, (int64_t)x->low); *p++ = ' '; p = put_i64(p, (int64_t)x->cap); *p++ = ' ';
+                p = put_i64(p, x->cost); *p++ = ' '; p = put_i64(p, x->type);
+                if (x->kind == 3) { *p++ = ' '; p = put_i64(p, x->old_cost); }
+                *p++ = '\n';
+                break;
+            default:
+                break;
+        }
+    }
+    p = put_s(p, "c EOI\n");
+    *p = 0;
+    return p - buf;
+}
+
+/* The daemon's side of that stream: parse the change block back into records
+ * until "c EOI". Returns the record count, or −1 on a malformed line. */
+int64_t ko_parse_changes(const char* text, int64_t len, ko_delta* out, int64_t cap) {
+    const char* p = text;
+    const char* e = text + len;
+    int64_t k = 0;
+    while (p < e) {
+        const char* le = memchr(p, '\n', (size_t)(e - p));
+        if (!le) le = e;
+        if (le > p) {
+            int ok = 1;
+            ko_delta x;
+            memset(&x, 0, sizeof(x));
+            int64_t v[7] = {0};
+            const char* q = p + 1;
+            if (*p == 'c') {
+                if (le - p == 5 && !strncmp(p, "c EOI", 5)) break;
+            } else if (*p == 'n') {
+                for (int i = 0; i < 3; ++i) q = get_i64(q, le, &v[i], &ok);
+                x.kind = 0; x.id = (uint64_t)v[0]; x.excess = v[1]; x.type = (int32_t)v[2];
+            } else if (*p == 'r') {
+                q = get_i64(q, le, &v[0], &ok);
+                x.kind = 1; x.id = (uint64_t)v[0];
+            } else if (*p == 'a' || *p == 'x') {
+                const int nf = *p == 'a' ? 6 : 7;
+                for (int i = 0; i < nf; ++i) q = get_i64(q, le, &v[i], &ok);
+                x.kind = *p == 'a' ? 2 : 3;
+                x.src = (uint64_t)v[0]; x.dst = (uint64_t)v[1]; x.low = (uint64_t)v[2]; x.cap = (uint64_t)v[3];
+                x.cost = v[4]; x.type = (int32_t)v[5]; x.old_cost = v[6];
+            } else {
+                ok = 0;
+            }
+            if (!ok) return -1;
+            if (*p != 'c') {
+                if (k < cap && out) out[k] = x;
+                ++k;
+            }
+        }
+        p = le + 1;
+    }
+    return k;
+}
+
+/* The reference path of a later Solve (solver.go:84-90): the change block as
+ * text and parsed back by the daemon, the incremental SSP re-solve, the "f"
+ * lines of every positive-flow arc, and the BFS mapping over them.
+ * ms[0..5] = export changes, parse, carry, saturate, augment, flines + bfs. */
+int ko_reference_path_incremental(const ko_graph* g, const ko_delta* deltas, int64_t k,
+                                  const int64_t* prev_src, const int64_t* prev_dst, const int64_t* prev_flow,
+                                  int64_t prev_m, const int64_t* prev_pot, int64_t prev_n, const uint8_t* fresh,
+                                  int64_t* flow_out, int64_t* pot_out, int64_t* total_cost, int64_t* flow_value,
+                                  int64_t* n_mapped, double* ms) {
+    const double t0 = now_ms();
+    const int64_t need = ko_export_changes(deltas, k, NULL, 0);
+    char* text = (char*)malloc((size_t)need + 1);
+    const int64_t tl = ko_export_changes(deltas, k, text, need + 1);
+    const double t1 = now_ms();
+    ko_delta* back = (ko_delta*)malloc(sizeof(ko_delta) * (size_t)(k + 1));
+    const int64_t kb = ko_parse_changes(text, tl, back, k + 1);
+    free(text);
+    free(back);
+    if (kb < 0) return -1;
+    const double t2 = now_ms();
+    double sm[3] = {0, 0, 0};
+    int64_t aug = 0;
+    const int st = ko_ssp_incremental(g, prev_src, prev_dst, prev_flow, prev_m, prev_pot, prev_n, fresh, flow_out,
+                                      pot_out, total_cost, flow_value, &aug, sm);
+    if (st < 0) return st;
+    const double t3 = now_ms();
+    const int64_t fneed = ko_flow_lines(g, flow_out, *total_cost, NULL, 0);
+    char* fl = (char*)malloc((size_t)fneed + 1);
+    const int64_t fll = ko_flow_lines(g, flow_out, *total_cost, fl, fneed + 1);
+    int64_t* tk = (int64_t*)malloc(sizeof(int64_t) * (g->n + 1));
+    int64_t* pu = (int64_t*)malloc(sizeof(int64_t) * (g->n + 1));
+    *n_mapped = ko_bfs_mapping_from_lines(g, fl, fll, tk, pu);
+    const double t4 = now_ms();
+    free(fl); free(tk); free(pu);
+    if (ms) {
+        ms[0] = t1 - t0; ms[1] = t2 - t1; ms[2] = sm[0]; ms[3] = sm[1]; ms[4] = sm[2]; ms[5] = t4 - t3;
+    }
+    (void)t3;
+    return st;
 }
 
 int ko_reference_path(const ko_graph* g, int64_t* total_cost, int64_t* flow_value,

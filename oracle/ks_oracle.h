@@ -31,6 +31,12 @@
  *   ko_bfs_mapping                   parseFlowToMapping + addPUToSourceNodes,
  *                                    placement/solver.go:183-269
  *   ko_reference_path                export → parse → SSP → f lines → parse → BFS
+ *   ko_ssp_incremental               SSP re-solve from the previous round's flow and
+ *                                    potentials (Flowlessly's daemon mode, which ksched
+ *                                    runs: solver.go:30-34 Incremental, :86-89)
+ *   ko_export_changes / ko_parse_changes   the ExportIncremental change block
+ *                                    (export.go:31-38, *_change.go GenerateChange)
+ *   ko_reference_path_incremental    change text → parse → incremental SSP → f lines → BFS
  */
 #ifndef KS_ORACLE_H
 #define KS_ORACLE_H
@@ -88,6 +94,34 @@ int64_t ko_bfs_mapping_from_lines(const ko_graph* g, const char* lines, int64_t 
 /* The whole reference CPU path; ms[0..4] = export, parse, ssp, flines, bfs. */
 int ko_reference_path(const ko_graph* g, int64_t* total_cost, int64_t* flow_value,
                       int64_t* n_mapped, double* ms);
+
+/* One change record (the same 72-byte layout as the product's ks_delta; kinds:
+ * 0 "n", 1 "r", 2 "a", 3 "x", 4 sink-excess drift with no line). */
+typedef struct ko_delta {
+    int32_t  kind, type;
+    uint64_t id, src, dst, low, cap;
+    int64_t  cost, old_cost, excess;
+} ko_delta;
+
+/* Incremental SSP re-solve (Flowlessly's daemon mode: solver.go:30-34, 86-89):
+ * the previous round's flow (by (src, dst)) and potentials (by node id; fresh
+ * nodes re-priced) are carried onto g, arcs the changes left with negative
+ * reduced cost are saturated, and SSP routes the resulting excess.
+ * pot_out (n) feeds the next round. ms[0..2] = carry, saturate, augment. */
+int ko_ssp_incremental(const ko_graph* g, const int64_t* prev_src, const int64_t* prev_dst,
+                       const int64_t* prev_flow, int64_t prev_m, const int64_t* prev_pot, int64_t prev_n,
+                       const uint8_t* fresh, int64_t* flow_out, int64_t* pot_out, int64_t* total_cost,
+                       int64_t* flow_value, int64_t* augmentations, double* ms);
+/* ExportIncremental text of a change block (export.go:31-38) and its parse. */
+int64_t ko_export_changes(const ko_delta* d, int64_t k, char* buf, int64_t cap);
+int64_t ko_parse_changes(const char* text, int64_t len, ko_delta* out, int64_t cap);
+/* A later Solve's reference path: change text → parse → incremental SSP →
+ * f lines → BFS. ms[0..5] = export, parse, carry, saturate, augment, flines+bfs. */
+int ko_reference_path_incremental(const ko_graph* g, const ko_delta* deltas, int64_t k,
+                                  const int64_t* prev_src, const int64_t* prev_dst, const int64_t* prev_flow,
+                                  int64_t prev_m, const int64_t* prev_pot, int64_t prev_n, const uint8_t* fresh,
+                                  int64_t* flow_out, int64_t* pot_out, int64_t* total_cost, int64_t* flow_value,
+                                  int64_t* n_mapped, double* ms);
 
 #ifdef __cplusplus
 }

@@ -72,3 +72,55 @@ def test_union_costs_split_per_graph():
     rec = np.zeros(pos.shape[0], [("src", "<u8"), ("dst", "<u8"), ("flow", "<i8")])
     rec["src"], rec["dst"], rec["flow"] = u.src[pos], u.dst[pos], fl[pos]
     assert batch.split_costs(u, noff, rec).tolist() == parts
+
+
+# --- the C-ABI gather layout (ks_batch.hip: ks_batch_owner / ks_batch_block_len /
+# ks_batch_unpack are the exact host functions ks_batch_load / ks_batch_gather use)
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_c_abi_row_layout_every_graph_lands_in_order(world):
+    """Every rank packs one block [status][rows] for the graphs it owns (as
+    ks_batch_gather does); rank 0 receives the blocks in rank order and unpacks
+    them: each graph's row must come back at its own index with its own content."""
+    from ksched_amd import native
+    ngraphs, max_tasks = 64, 5
+    block = native.batch_block_len(ngraphs, world, max_tasks)
+    slots = -(-ngraphs // world)
+    assert block == 1 + slots * (2 + max_tasks)
+    gathered = np.zeros(world * block, np.int64)
+    owned = {r: [] for r in range(world)}
+    for g in range(ngraphs):
+        r, sl = native.batch_owner(g, world)
+        assert r == g % world and sl == g // world     # round-robin (SURVEY §8d config 5)
+        owned[r].append(g)
+        assert owned[r].index(g) == sl                 # slot = position among the rank's graphs
+    for r, gs in owned.items():                        # each rank packs its own block
+        for sl, g in enumerate(gs):
+            row = r * block + 1 + sl * (2 + max_tasks)
+            gathered[row] = 1000 + g                   # cost
+            gathered[row + 1] = 2000 + g               # flow
+            gathered[row + 2:row + 2 + max_tasks] = 10 * g + np.arange(max_tasks)
+    pu, cost, flow = native.batch_unpack(gathered, ngraphs, world, max_tasks)
+    assert cost.tolist() == [1000 + g for g in range(ngraphs)]
+    assert flow.tolist() == [2000 + g for g in range(ngraphs)]
+    for g in range(ngraphs):
+        assert pu[g].tolist() == [10 * g + k for k in range(max_tasks)]
+
+
+def test_c_abi_unpack_reports_a_failed_rank():
+    from ksched_amd import native
+    ngraphs, world, max_tasks = 8, 4, 3
+    block = native.batch_block_len(ngraphs, world, max_tasks)
+    gathered = np.zeros(world * block, np.int64)
+    gathered[2 * block] = native.KS_E_INVALID          # rank 2's status word
+    with pytest.raises(native.KsError) as e:
+        native.batch_unpack(gathered, ngraphs, world, max_tasks)
+    assert e.value.code == native.KS_E_INVALID
+
+
+def test_c_abi_layout_matches_python_sharding():
+    """The Python helpers (bench / torch.distributed path) and the C-ABI agree."""
+    from ksched_amd import native
+    for world in (1, 2, 4, 8):
+        for g in range(64):
+            assert native.batch_owner(g, world) == batch.owner(g, world)
+        assert native.load().ks_batch_slots(64, world) == batch.slots_per_rank(64, world)

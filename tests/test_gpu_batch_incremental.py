@@ -220,10 +220,12 @@ def test_deltas_applied_in_place_on_device():
         assert sum(rebuilt[1:]) <= 3, rebuilt  # then the slack absorbs most rounds
 
 
-def test_batch_c_abi_rccl_gather():
+def test_batch_c_abi_gather_world1():
     """Config 5 through the C-ABI (ks_batch_*: the disjoint union per device,
-    per-graph rows gathered to rank 0 over RCCL inside libksmcmf) on the box's
-    one device: per-graph cost and flow vs the oracle, cell-local PU ids valid."""
+    per-graph rows packed as for the RCCL gather) at world size 1 — the one
+    device of the box, so no RCCL call is made (the multi-rank layout is covered
+    on the CPU by tests/test_batch_cpu.py): per-graph cost and flow vs the
+    oracle, cell-local PU ids valid."""
     T, M, R, J = 3_000, 300, 12, 30
     graphs = [gen.quincy(T, M, R, J, 1200 + i) for i in range(6)]
     b = native.Batch(devices=[0])

@@ -276,20 +276,63 @@ def test_mapping_with_flow_cycles_terminates_and_respects_pus(ctx):
         check_mapping(g, ctx.task_mapping())
 
 
-@pytest.mark.parametrize("env", [{"KS_AUG": "0"}, {"KS_AUG_SLACK": "1"}, {"KS_AUG_SLACK": "4", "KS_TAIL_GI": "2"}])
-def test_tail_walks_do_not_change_the_optimum(ctx, monkeypatch, env):
+@pytest.mark.parametrize("opts", [{"walk_slack": -1}, {"walk_slack": 1}, {"walk_slack": 4, "tail_sweeps": 2}])
+def test_tail_walks_do_not_change_the_optimum(opts):
     """The phase-tail walks (k_augment / k_aug_hub) off, at slack 1
-    (ε-optimality kept) and at the default slack with the fewest tail sweeps: the
-    same optimal cost and flow, the flow re-verified by the oracle — on a
-    config-2-sized Quincy cell (hub excess in every phase's tail) and on random
-    graphs with several deficits, lower bounds and parallel paths."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)      # read by the engine at every ks_solve
-    g = gen.quincy(10_000, 1_000, 25, 100, 2)
-    st, c, fv, _, _ = ko.ssp(g)
-    assert st == 0
-    solve_and_check(ctx, g, c, fv)
-    for trial, g in random_graphs(777, 15):
+    (ε-optimality kept) and at the default slack with the fewest tail sweeps —
+    set through ks_opts, not the environment: the same optimal cost and flow, the
+    flow re-verified by the oracle — on a config-2-sized Quincy cell (hub excess
+    in every phase's tail) and on random graphs with several deficits, lower
+    bounds and parallel paths."""
+    with native.Context(0, **opts) as c2:
+        g = gen.quincy(10_000, 1_000, 25, 100, 2)
         st, c, fv, _, _ = ko.ssp(g)
-        if st == 0:
-            solve_and_check(ctx, g, c, fv)
+        assert st == 0
+        solve_and_check(c2, g, c, fv)
+        for trial, g in random_graphs(777, 15):
+            st, c, fv, _, _ = ko.ssp(g)
+            if st == 0:
+                solve_and_check(c2, g, c, fv)
+
+
+@pytest.mark.parametrize("fault", [1, 2])
+def test_failed_certificate_is_recovered(fault):
+    """A failed final optimality certificate is repaired, not fatal
+    (replaces the panic of placement/solver.go:223-225 on a bad solve):
+    fault 1 — with price refinement off the ladder runs down to ε = 1 and the
+    last phase's walks use the coarse slack (the flow may end 4-optimal only);
+    fault 2 — an optimal flow whose prices are perturbed before verification.
+    Either way the solve returns the oracle's cost, the flow re-verified, and
+    fault 2 always needs (and counts) a recovery."""
+    opts = {"fault_inject": fault}
+    if fault == 1:
+        opts["price_refine"] = 0
+    with native.Context(0, **opts) as c2:
+        for g in (gen.quincy(10_000, 1_000, 25, 100, 2), gen.quincy(3_000, 300, 12, 30, 10)):
+            st, c, fv, _, _ = ko.ssp(g)
+            r = solve_and_check(c2, g, c, fv)
+            if fault == 2:
+                assert r.raw["recoveries"] >= 1
+            assert r.raw["recoveries"] <= 2
+
+
+def test_failed_load_leaves_the_context_usable(ctx):
+    """a load rejected for a bad arc changes nothing (host table and
+    device store); a later apply + solve works on the previous graph."""
+    g = gen.quincy(1_000, 100, 5, 10, 1)
+    st, c, fv, _, _ = ko.ssp(g)
+    ctx.load_graph(g)
+    r = ctx.solve()
+    assert (r.cost, r.flow) == (c, fv)
+    nodes, arcs = native.graph_arrays(gen.quincy(500, 50, 5, 10, 9))
+    arcs[3]["dst"] = 10 ** 6                      # an endpoint that does not exist
+    with pytest.raises(native.KsError) as e:
+        ctx.load_arrays(nodes, arcs)
+    assert e.value.code == native.KS_E_INVALID
+    d = np.zeros(1, native.DELTA_DT)              # a no-op upsert of an existing arc
+    d[0]["kind"] = native.KS_ADD_ARC
+    d[0]["src"], d[0]["dst"], d[0]["cap"], d[0]["cost"] = g.src[0], g.dst[0], g.cap[0], g.cost[0]
+    ctx.apply_deltas(d)
+    r = ctx.solve()
+    assert (r.cost, r.flow) == (c, fv)
+    check_mapping(g, ctx.task_mapping())
