@@ -205,7 +205,16 @@ class Dist:
 
 
 def opts_of(args) -> dict:
+    """ks_opts for the bench's contexts: the flags below, plus --opt key=value (any
+    ks_opts field; also KS_BENCH_OPTS="key:value+key:value" for A/B scripts)."""
     o = {}
+    pairs = list(args.opt or [])
+    env = os.environ.get("KS_BENCH_OPTS")
+    if env:
+        pairs += [p.replace(":", "=") for p in env.split("+") if p]
+    for kv in pairs:
+        k, v = kv.split("=", 1)
+        o[k.strip()] = int(v)
     if args.alpha:
         o["alpha"] = args.alpha
     if args.gu_interval:
@@ -574,6 +583,7 @@ def main():
     ap.add_argument("--alpha", type=int, default=0)
     ap.add_argument("--gu-interval", type=int, default=0)
     ap.add_argument("--price-refine", type=int, default=-1)
+    ap.add_argument("--opt", action="append", help="ks_opts field=value (repeatable)")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 10 if args.workload == "incremental" else 5    # config 4 is 10 rounds

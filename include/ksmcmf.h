@@ -95,8 +95,9 @@ typedef struct ks_opts {
                                   scratch (faster on config 4)      */
     /* solver tuning; 0 selects the library default given in brackets.
        None of these changes the result — only how fast it is reached. */
-    int32_t  walk_slack;       /* a phase's tail walks take residual arcs of reduced cost
-                                  ≤ walk_slack·ε while ε > 1 [4]; < 0 disables the walks */
+    int32_t  walk_slack;       /* a phase's tail walkers take residual arcs of reduced cost
+                                  ≤ walk_slack·ε toward a smaller distance while ε > 1
+                                  [4]; < 0 disables the walkers                       */
     int32_t  final_div;        /* the phase price refinement certifies runs at 1/final_div
                                   of a cost unit [48]; < 0: the plain max|cost|/α^k ladder */
     int32_t  pr_rounds;        /* Bellman-Ford rounds one price refinement may take [160] */
@@ -114,7 +115,11 @@ typedef struct ks_opts {
                                   coarse slack at ε = 1 (may end non-1-optimal); bit 1 —
                                   the final prices are perturbed before verification.
                                   Both must be repaired by the certificate recovery.    */
-    int32_t  reserved[8];
+    int32_t  walk_passes;      /* blocking-flow walker passes per tail cycle [1]         */
+    int32_t  tail_nodes;       /* a phase's tail — blocking flows over each update, few
+                                  sweeps — starts once ≤ tail_nodes nodes hold excess
+                                  [64]; at most 4096                                    */
+    int32_t  reserved[6];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */

@@ -40,10 +40,11 @@
 //              inbox; hub chunks claim excess with a CAS and the last-arriving
 //              chunk finalises the relabel. Bellman-Ford relaxations into a hub
 //              are min-reduced in LDS per workgroup.
-//   tail       once an update leaves ≤ 64 nodes with excess, each sends its
-//              units down the update's distances to a deficit in one kernel
-//              (k_augment walks; k_aug_hub hands a hub's excess on in parallel)
-//              instead of one hop per sweep over dozens of update cycles.
+//   tail       once an update leaves ≤ 64 nodes with excess, a blocking flow
+//              over the update's distances (k_dfs_walk: one DFS walker per
+//              source with shared dead-end marks, hub excess split over many
+//              walkers via k_hub_cands) routes most of the remaining units in
+//              one kernel instead of one hop per sweep over dozens of cycles.
 //   verify     on-device: conservation, capacity, and 1-optimality of the final
 //              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
 //              the total cost is reduced in int64.
@@ -100,12 +101,7 @@ constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp (DE
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7 };
-#ifndef KS_AUG_K
-#define KS_AUG_K 64                 // a phase's tail: at most this many excess nodes are augmented directly
-#endif
-constexpr int AUG_K = KS_AUG_K;
-constexpr int AUG_K2 = 256;        // walkers from the nodes a hub distribution fed
-constexpr int AUG_STEPS = 512;     // hops per walk before its units are left where it stands
+constexpr int AUG_KMAX = 4096;     // most excess nodes a tail's walkers start from (ks_opts.tail_nodes)
 
 struct Ctl {
     long long eps;
@@ -123,7 +119,6 @@ struct Ctl {
     int bf_seq0;           // sequence number of the running update's first (dense) round
     int aug_reached;       // walks of this cycle that reached a deficit / stopped short
     int aug_short;
-    int n_xl2;             // nodes fed by this cycle's hub distribution
     int dbg_x[4];          // diagnostics (KS_CYCLE_LOG): the first listed excess nodes, their excess at the apply
     int dbg_e[4];
 };
@@ -161,11 +156,7 @@ struct DG {
     int hub_base;
     int expand;            // Bellman-Ford: relax low-degree targets two hops per round
     const int* first;
-    const int* head;
-    const int* rev;
-    long long* rcap;
-    const long long* ucap;   // rcap(a) + rcap(rev a), constant
-    const long long* cost;
+    Pos* pos;              // residual positions: cost, rcap, ucap = rcap(a) + rcap(rev a), head, rev
     long long* excess;
     long long* p0;         // node records (stride 4, index with ni()): p0 at +0, dist at +1, p1 at +2
     long long* p1;
@@ -182,9 +173,12 @@ struct DG {
     int ncls_c;            // nodes of the chunked class
     int sw_clsb;           // sweep blocks striding the class windows (after the hub blocks)
     const int* hnchunks;
-    int* xl;               // excess nodes listed by the last apply (the first AUG_K)
-    int* xl2;              // nodes fed by k_aug_hub (the first AUG_K2)
-    long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
+    int* xl;               // excess nodes listed by the last apply (the first aug_k)
+    int aug_k;             // a phase's tail: ≤ aug_k excess nodes (ks_opts.tail_nodes)
+    int* dead;             // per node: the walk stamp of the cycle that found it a dead end
+    int* hub_cand;         // per hub: qualifying out-arc positions (k_hub_cands), HC_CAP each
+    int* hub_cnt;          // per hub: entries listed this cycle
+    long long* hub_e;      // per hub: its excess when listed (the walkers' split)
     long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
     long long* q_taken;
     long long* q_min;
@@ -236,7 +230,23 @@ __device__ __forceinline__ void atom_min(long long* p, long long v) {
 __device__ __forceinline__ long long atom_load(const long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ int atom_load_i(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One residual position (ks_pos.h) in two 16-byte loads issued together.
+__device__ __forceinline__ Pos ld_pos(const Pos* p) {
+    const longlong2 a = reinterpret_cast<const longlong2*>(p)[0];   // cost, rcap
+    const longlong2 b = reinterpret_cast<const longlong2*>(p)[1];   // ucap, head | rev << 32
+    Pos r;
+    r.cost = a.x;
+    r.rcap = a.y;
+    r.ucap = b.x;
+    r.head = (int)(unsigned)((unsigned long long)b.y & 0xffffffffULL);
+    r.rev = (int)(unsigned)((unsigned long long)b.y >> 32);
+    return r;
+}
 
 // ------------------------------------------------------------ wave helpers ---
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
@@ -331,11 +341,11 @@ __device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
 __device__ __forceinline__ void push_arc(const DG& g, const Front* nf, int a, int w, long long r, long long d,
                                          Pend& pd, int& out, int rv = -1, long long uc = 0) {
     if (rv < 0) {
-        rv = g.rev[a];
-        uc = g.ucap[a];
+        rv = g.pos[a].rev;
+        uc = g.pos[a].ucap;
     }
-    g.rcap[a] = r - d;
-    g.rcap[rv] = uc - (r - d);
+    g.pos[a].rcap = r - d;
+    g.pos[rv].rcap = uc - (r - d);
     if (w < g.hub_base) {
         atom_add(&g.excess[w], d);
         if (nf) {
@@ -577,21 +587,16 @@ __global__ void k_first(int nn, long long m2, const unsigned* __restrict__ keys,
 }
 
 // Every position inert, owned by the node whose segment holds it.
-__global__ void k_inert_all(long long m2cap, int nn, const int* __restrict__ first, int* __restrict__ head,
-                            int* __restrict__ rev, int* __restrict__ ent, long long* __restrict__ rcap,
-                            long long* __restrict__ ucap, long long* __restrict__ scost) {
+__global__ void k_inert_all(long long m2cap, int nn, const int* __restrict__ first, Pos* __restrict__ pos,
+                            int* __restrict__ ent) {
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2cap; p += (long long)gridDim.x * BLK) {
         int lo = 0, hi = nn;   // owner: the last v with first[v] <= p
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
             if (first[mid] <= p) lo = mid; else hi = mid;
         }
-        head[p] = lo;
-        rev[p] = (int)p;
+        pos[p] = Pos{DEAD_COST, 0, 0, lo, (int)p};
         ent[p] = -1;
-        rcap[p] = 0;
-        ucap[p] = 0;
-        scost[p] = DEAD_COST;
     }
 }
 
@@ -599,8 +604,7 @@ __global__ void k_fill_csr(long long m2, int nn, const unsigned* __restrict__ ke
                            const int* __restrict__ rs, const int* __restrict__ first, const int* __restrict__ perm,
                            const int* __restrict__ src, const int* __restrict__ dst, const long long* __restrict__ low,
                            const long long* __restrict__ cap, const long long* __restrict__ cost, long long mult,
-                           int* __restrict__ head, long long* __restrict__ rcap, long long* __restrict__ ucap,
-                           long long* __restrict__ scost, int* __restrict__ ent, int* __restrict__ fwd,
+                           Pos* __restrict__ pos, int* __restrict__ ent, int* __restrict__ fwd,
                            int* __restrict__ pos_of) {
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m2; i += (long long)gridDim.x * BLK) {
         const int v = (int)keys[i];
@@ -610,22 +614,22 @@ __global__ void k_fill_csr(long long m2, int nn, const unsigned* __restrict__ ke
         const int s = val >> 1;
         const bool r = val & 1;
         pos_of[val] = p;
-        head[p] = perm[r ? src[s] : dst[s]];
         const long long u = cap[s] - low[s];
-        rcap[p] = r ? 0 : u;
-        ucap[p] = u;
-        scost[p] = (r ? -cost[s] : cost[s]) * mult;
+        pos[p].head = perm[r ? src[s] : dst[s]];
+        pos[p].rcap = r ? 0 : u;
+        pos[p].ucap = u;
+        pos[p].cost = (r ? -cost[s] : cost[s]) * mult;
         ent[p] = val;
         if (!r) fwd[s] = p;
     }
 }
 
 __global__ void k_fill_rev(long long m2, int nn, const unsigned* __restrict__ keys, const int* __restrict__ vals,
-                           const int* __restrict__ pos_of, int* __restrict__ rev) {
+                           const int* __restrict__ pos_of, Pos* __restrict__ pos) {
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < m2; i += (long long)gridDim.x * BLK) {
         if ((int)keys[i] >= nn) continue;
         const int val = vals[i];
-        rev[pos_of[val]] = pos_of[val ^ 1];
+        pos[pos_of[val]].rev = pos_of[val ^ 1];
     }
 }
 
@@ -637,11 +641,10 @@ __global__ void k_used(int nn, const int* __restrict__ rs, int* __restrict__ use
 // ------------------------------------------------------------ cold reset ---
 // Zero flow: forward residual = u, reverse 0; excess = supply with the
 // lower-bound transform; prices 0. Runs before every cold solve (no rebuild).
-__global__ void k_reset_pos(long long m2cap, const int* __restrict__ ent, const long long* __restrict__ ucap,
-                            long long* __restrict__ rcap) {
+__global__ void k_reset_pos(long long m2cap, const int* __restrict__ ent, Pos* __restrict__ pos) {
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2cap; p += (long long)gridDim.x * BLK) {
         const int e = ent[p];
-        if (e >= 0) rcap[p] = (e & 1) ? 0 : ucap[p];
+        if (e >= 0) pos[p].rcap = (e & 1) ? 0 : pos[p].ucap;
     }
 }
 
@@ -715,11 +718,12 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            const long long r = g.rcap[a];
+            const Pos q = ld_pos(g.pos + a);
+            const long long r = q.rcap;
             if (r > 0) {
-                const int w = g.head[a];
-                if (g.cost[a] + pv - P[ni(w)] < -thr) {
-                    push_arc(g, nullptr, a, w, r, r, pd, out);
+                const int w = q.head;
+                if (q.cost + pv - P[ni(w)] < -thr) {
+                    push_arc(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
                     tot += r;
                     c.push++;
                 }
@@ -747,11 +751,12 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
         for (int k = 0; k < PER_T; ++k) {
             const int a = it.begin + threadIdx.x * PER_T + k;
             if (a < it.end) {
-                const long long r = g.rcap[a];
+                const Pos q = ld_pos(g.pos + a);
+                const long long r = q.rcap;
                 if (r > 0) {
-                    const int w = g.head[a];
-                    if (g.cost[a] + px - P[ni(w)] < -thr) {
-                        push_arc(g, nullptr, a, w, r, r, pd, out);
+                    const int w = q.head;
+                    if (q.cost + px - P[ni(w)] < -thr) {
+                        push_arc(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
                         tot += r;
                         c.push++;
                     }
@@ -794,11 +799,12 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         int rv = 0;
         long long uc = 0;
         if (valid) {
-            r = g.rcap[a];
-            w = g.head[a];
-            rv = g.rev[a];     // issued with the arc: a push needs no further load
-            uc = g.ucap[a];
-            cr = g.cost[a] + pv - P[ni(w)];
+            const Pos q = ld_pos(g.pos + a);   // the whole record: a push needs no further load
+            r = q.rcap;
+            w = q.head;
+            rv = q.rev;
+            uc = q.ucap;
+            cr = q.cost + pv - P[ni(w)];
             c.scan++;
         }
         const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
@@ -907,19 +913,21 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
         w[k] = 0;
         rv[k] = 0;
         uc[k] = 0;
+        cr[k] = 0;
         if (a < it.end) {
-            r[k] = g.rcap[a];
-            w[k] = g.head[a];
-            rv[k] = g.rev[a];
-            uc[k] = g.ucap[a];
+            const Pos q = ld_pos(g.pos + a);
+            r[k] = q.rcap;
+            w[k] = q.head;
+            rv[k] = q.rev;
+            uc[k] = q.ucap;
+            cr[k] = q.cost;   // + px − P[head], below
         }
     }
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
         const int a = it.begin + threadIdx.x * PER_T + k;
-        cr[k] = 0;
         if (a < it.end) {
-            cr[k] = g.cost[a] + px - P[ni(w[k])];
+            cr[k] += px - P[ni(w[k])];
             c.scan++;
         }
         adm[k] = (a < it.end && cr[k] < 0 && r[k] > 0) ? r[k] : 0;
@@ -985,12 +993,13 @@ __device__ void node_discharge(const DG& g, const Front& F, const Front& N, int 
             w[j] = 0;
             rv[j] = 0;
             uc[j] = 0;
-            if (a < en) {   // reverse position and pair capacity too: a push needs no further load
-                r[j] = g.rcap[a];
-                w[j] = g.head[a];
-                cs[j] = g.cost[a];
-                rv[j] = g.rev[a];
-                uc[j] = g.ucap[a];
+            if (a < en) {   // the whole record: a push needs no further load
+                const Pos q = ld_pos(g.pos + a);
+                r[j] = q.rcap;
+                w[j] = q.head;
+                cs[j] = q.cost;
+                rv[j] = q.rev;
+                uc[j] = q.ucap;
             }
         }
 #pragma unroll
@@ -1066,11 +1075,12 @@ __device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, 
             rv[j] = 0;
             uc[j] = 0;
             if (a < en) {
-                r[j] = g.rcap[a];
-                w[j] = g.head[a];
-                cs[j] = g.cost[a];
-                rv[j] = g.rev[a];
-                uc[j] = g.ucap[a];
+                const Pos q = ld_pos(g.pos + a);
+                r[j] = q.rcap;
+                w[j] = q.head;
+                cs[j] = q.cost;
+                rv[j] = q.rev;
+                uc[j] = q.ucap;
             }
         }
 #pragma unroll
@@ -1142,12 +1152,21 @@ __device__ __forceinline__ int class_of_window(const DG& g, int w) {
 // clears what was set (class windows only; a chunk item's flag is cleared by
 // the node's owner) and ballots it — nothing when go is false.
 struct WinFlag {
-    int slot;   // flag index this lane read (-1: none)
-    int raw;    // the flag byte
+    int slot;        // flag index this lane read (-1: none)
+    int raw;         // the flag byte
+    long long a;     // KS_PREFETCH, class windows: loaded WITH the flag — sweeps: the node's
+    long long p;     //   excess and price (read buffer); Bellman-Ford: its distance and p0;
+    long long seg;   //   both: its packed segment bounds (one dependent step fewer per launch)
 };
-__device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char* flags, int w) {
+#ifndef KS_PREFETCH
+#define KS_PREFETCH 1
+#endif
+// MODE 0: the flag only; 1: sweep (excess, P); 2: Bellman-Ford (dist, p0).
+template <int MODE>
+__device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char* flags, int w,
+                                               const long long* P = nullptr) {
     w = __builtin_amdgcn_readfirstlane(w);   // wave-uniform: the class selection stays scalar
-    WinFlag f{-1, 0};
+    WinFlag f{-1, 0, 0, 0, 0};
     const int ln = lane_id();
     if (w < g.wbeg[CCLS]) {
         // class c = the last with wbeg[c] <= w, selected over static fields (kernel
@@ -1161,6 +1180,16 @@ __device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char*
                 ws = win_slots(k);
             }
         if (ln < ws) f.slot = ob + (w - wb) * ws + ln;
+        if (KS_PREFETCH && MODE && f.slot >= 0) {
+            f.seg = g.p0[ni(f.slot) + ND_SEG];
+            if (MODE == 1) {
+                f.a = atom_load(&g.excess[f.slot]);
+                f.p = P[ni(f.slot)];
+            } else {
+                f.a = atom_load(&g.dist[ni(f.slot)]);
+                f.p = g.p0[ni(f.slot)];
+            }
+        }
     } else if (w < g.wbeg[CCLS] + g.ncitems) {
         if (ln == 0) f.slot = g.citems[w - g.wbeg[CCLS]].node;
     }
@@ -1173,6 +1202,16 @@ __device__ __forceinline__ unsigned long long window_take(const DG& g, unsigned 
     if (on && w < g.wbeg[CCLS]) flags[f.slot] = 0;
     return __ballot(on);
 }
+// The prefetched record of node v (v − base = the lane that loaded it), to every lane.
+__device__ __forceinline__ void window_node(const WinFlag& f, int v, int base, long long& a, long long& p, int& b0,
+                                            int& en) {
+    const int src = v >= 0 ? v - base : 0;
+    a = __shfl(f.a, src);
+    p = __shfl(f.p, src);
+    const unsigned long long sg = (unsigned long long)__shfl(f.seg, src);
+    b0 = (int)(unsigned)(sg & 0xffffffffULL);
+    en = (int)(unsigned)(sg >> 32);
+}
 
 // The control words of a launch pass through an empty asm that also takes the
 // launch's first loads as inputs: the words are only tested after every one of
@@ -1182,8 +1221,8 @@ __device__ __forceinline__ unsigned long long window_take(const DG& g, unsigned 
 
 template <int C>
 __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, unsigned long long mask,
-                                          const long long* __restrict__ P, long long* __restrict__ PN, long long eps,
-                                          Pend& pd, int& out, Cnt& c) {
+                                          const WinFlag& f, const long long* __restrict__ P,
+                                          long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
     constexpr int G = class_lanes(C);
     constexpr int PER = 64 / G;
     constexpr int WS = win_slots(C);
@@ -1195,11 +1234,14 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
         long long e = 0, pv = 0;
         int b0 = 0, en = 0;
-        if (v >= 0) {
+        if (KS_PREFETCH) {
+            window_node(f, v, base, e, pv, b0, en);
+        } else if (v >= 0) {
             e = atom_load(&g.excess[v]);
             pv = P[ni(v)];
             seg_of(g.p0, v, b0, en);
         }
+        if (v < 0) e = 0;
         sweep_group<G>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
@@ -1310,7 +1352,7 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
             const int w = w0 + j * tw;
-            wf[j] = w < g.wbeg[CCLS] ? window_load(g, F.flag, w) : WinFlag{-1, 0};
+            wf[j] = w < g.wbeg[CCLS] ? window_load<1>(g, F.flag, w, P) : WinFlag{-1, 0, 0, 0, 0};
             any_raw |= wf[j].raw;
         }
         ctl_words();
@@ -1327,11 +1369,11 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             kind = max(kind, 3 + class_of_window(g, w));
 #endif
             switch (class_of_window(g, w)) {
-                case 0: sweep_win<0>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
-                case 1: sweep_win<1>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
-                case 2: sweep_win<2>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
-                case 3: sweep_win<3>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
-                default: sweep_win<4>(g, N, w, mk[j], P, PN, eps, pd, out, c); break;
+                case 0: sweep_win<0>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 1: sweep_win<1>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 2: sweep_win<2>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 3: sweep_win<3>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                default: sweep_win<4>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
             }
         }
     }
@@ -1387,35 +1429,112 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 
 // Relax the in-arcs of a low-degree node u (≤ 8 arcs: tasks, PUs) right after
 // its distance dropped to du: a second hop inside the same round.
+#ifndef KS_HOP3
+#define KS_HOP3 0
+#endif
 template <bool PR>
+__device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
+                           long long* hub_min, int& out);
+
+template <bool PR, bool MID = (KS_HOP3 != 0)>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
                                             int b0, int b1, long long eps, long long* hub_min, int& out) {
-    // residual tests of all (≤ 8) arcs issued together; usually one in-arc carries
+    // the records of all (≤ 8) arcs issued together; usually one in-arc carries
     // flow (a task's assignment), so the dependent loads follow for it alone
     unsigned live = 0;
+    int hd[8];
+    long long cb[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (b0 + k < b1 && g.ucap[b0 + k] - g.rcap[b0 + k] > 0) live |= 1u << k;
+    for (int k = 0; k < 8; ++k) {
+        hd[k] = 0;
+        cb[k] = 0;
+        if (b0 + k < b1) {
+            const Pos q = ld_pos(g.pos + b0 + k);
+            hd[k] = q.head;
+            cb[k] = q.cost;
+            if (q.ucap - q.rcap > 0) live |= 1u << k;
+        }
+    }
     for (int b = b1 - b0 > 8 ? b0 + 8 : b1; b < b1; ++b)   // leaves have ≤ 8 arcs; kept for safety
-        if (g.ucap[b] - g.rcap[b] > 0) {
-            const int u2 = g.head[b];
-            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], g.cost[b], pu, eps);
+        if (g.pos[b].ucap - g.pos[b].rcap > 0) {
+            const int u2 = g.pos[b].head;
+            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], g.pos[b].cost, pu, eps);
             if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
             }
         }
     while (live) {
-        const int b = b0 + __builtin_ctz(live);
+        const int k = __builtin_ctz(live);
         live &= live - 1;
-        const int u2 = g.head[b];
-        const long long cb = g.cost[b];
+        int u2 = 0;
+        long long c2 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)   // register select (no dynamic indexing into scratch)
+            if (j == k) {
+                u2 = hd[j];
+                c2 = cb[j];
+            }
         const long long pu2 = g.p0[ni(u2)];
         const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
-        const long long cand = du + arc_len<PR>(pu2, cb, pu, eps);
+        const long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
         if (offer<PR>(g, nf, u2, cand, du2, hub_min, out)) {
-            nf.flag[u2] = 1;
-            out = 1;
+            if (MID && u2 >= g.obeg[2] && u2 < g.obeg[4]) {
+                expand_mid<PR>(g, nf, u2, cand, pu2, eps, hub_min, out);   // a machine: two more hops
+            } else {
+                nf.flag[u2] = 1;
+                out = 1;
+            }
+        }
+    }
+}
+
+// KS_HOP3: a mid-degree node (≤ 32 arcs: machines) reached through a leaf relaxes
+// its own in-arcs at once, and the leaves it lowers (tasks) theirs: an alternating
+// machine ← task ← machine ← task path advances two displacements per round.
+template <bool PR>
+__device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
+                           long long* hub_min, int& out) {
+    int b0, b1;
+    seg_of(g.p0, u, b0, b1);
+    for (int base = b0; base < b1; base += 8) {
+        unsigned live = 0;
+        int hd[8];
+        long long cb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            hd[k] = 0;
+            cb[k] = 0;
+            if (base + k < b1) {
+                const Pos q = ld_pos(g.pos + base + k);
+                hd[k] = q.head;
+                cb[k] = q.cost;
+                if (q.ucap - q.rcap > 0) live |= 1u << k;
+            }
+        }
+        while (live) {
+            const int k = __builtin_ctz(live);
+            live &= live - 1;
+            int u3 = 0;
+            long long c3 = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j == k) {
+                    u3 = hd[j];
+                    c3 = cb[j];
+                }
+            const long long pu3 = g.p0[ni(u3)];
+            const long long du3 = u3 < g.hub_base ? g.dist[ni(u3)] : INF64;
+            const long long cand = du + arc_len<PR>(pu3, c3, pu, eps);
+            if (!offer<PR>(g, nf, u3, cand, du3, hub_min, out)) continue;
+            if (g.expand && u3 < g.obeg[2]) {
+                int e0, e1;
+                seg_of(g.p0, u3, e0, e1);
+                expand_leaf<PR, false>(g, nf, u3, cand, pu3, e0, e1, eps, hub_min, out);
+            } else {
+                nf.flag[u3] = 1;
+                out = 1;
+            }
         }
     }
 }
@@ -1425,9 +1544,10 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
 template <bool PR>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
                                          long long eps, long long* hub_min, int& out) {
-    const long long rin = g.ucap[a] - g.rcap[a];
-    const int u = g.head[a];
-    const long long ca = g.cost[a];
+    const Pos q = ld_pos(g.pos + a);
+    const long long rin = q.ucap - q.rcap;
+    const int u = q.head;
+    const long long ca = q.cost;
     const long long pu = g.p0[ni(u)];
     const long long du = u < g.hub_base ? g.dist[ni(u)] : INF64;
     const bool leaf = g.expand && u < g.obeg[2];
@@ -1462,8 +1582,8 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
 
 // Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
 template <int C, bool PR>
-__device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, long long eps,
-                                       long long* hub_min, int& out, long long& scans) {
+__device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, const WinFlag& f,
+                                       long long eps, long long* hub_min, int& out, long long& scans) {
     constexpr int G = class_lanes(C);
     constexpr int PER = 64 / G;
     constexpr int WS = win_slots(C);
@@ -1475,11 +1595,14 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
         long long d = INF64, pv = 0;
         int b0 = 0, en = 0;
-        if (v >= 0) {
+        if (KS_PREFETCH) {
+            window_node(f, v, base, d, pv, b0, en);
+        } else if (v >= 0) {
             d = atom_load(&g.dist[ni(v)]);
             pv = g.p0[ni(v)];
             seg_of(g.p0, v, b0, en);
         }
+        if (v < 0) d = INF64;
         bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, hub_min, out, scans);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
@@ -1594,7 +1717,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         int any_raw = 0;
 #pragma unroll
         for (int j = 0; j < WPW; ++j) {
-            wf[j] = window_load(g, F.flag, w0 + j * tw);
+            wf[j] = window_load<2>(g, F.flag, w0 + j * tw);
             any_raw |= wf[j].raw;
         }
         ctl_words();
@@ -1627,11 +1750,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             kind = max(kind, 3 + class_of_window(g, w));
 #endif
             switch (class_of_window(g, w)) {
-                case 0: bf_win<0, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
-                case 1: bf_win<1, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
-                case 2: bf_win<2, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
-                case 3: bf_win<3, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
-                default: bf_win<4, PR>(g, N, w, mk[j], eps, hub_min, out, scans); break;
+                case 0: bf_win<0, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
+                case 1: bf_win<1, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
+                case 2: bf_win<2, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
+                case 3: bf_win<3, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
+                default: bf_win<4, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
             }
         }
     }
@@ -1748,10 +1871,12 @@ __global__ void k_gu_max(DG g) {
     clear_fronts(g, g.sf);
     if (blockIdx.x == 0) {
         for (int k = threadIdx.x; k < MAXB; k += BLK) g.ctl->sweep_act[k] = 0;
-        for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.aug_req[h] = 0;
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) {
+            g.hub_cnt[h] = 0;
+            g.hub_e[h] = 0;
+        }
         if (threadIdx.x == 0) {
             g.ctl->apply_act = 0;
-            g.ctl->n_xl2 = 0;
         }
     }
     if (!g.ctl->bf_done) return;
@@ -1793,7 +1918,7 @@ __global__ void k_gu_apply(DG g, int sseq) {
             xv = (int)v;
         }
     }
-    // count the excess nodes (one atomic per wave) and list the first AUG_K for k_augment
+    // count the excess nodes (one atomic per wave) and list the first aug_k for the walkers
     const unsigned long long ex = __ballot(out);
     int base = 0;
     if (ex && lane_id() == 0) {
@@ -1803,7 +1928,7 @@ __global__ void k_gu_apply(DG g, int sseq) {
     base = __shfl(base, 0);
     if (out) {
         const int idx = base + (int)__popcll(ex & ((1ULL << lane_id()) - 1));
-        if (idx < AUG_K) g.xl[idx] = xv;
+        if (idx < g.aug_k) g.xl[idx] = xv;
         if (idx < 4) {
             g.ctl->dbg_x[idx] = xv;
             g.ctl->dbg_e[idx] = (int)atom_load(&g.excess[xv]);
@@ -1811,206 +1936,227 @@ __global__ void k_gu_apply(DG g, int sseq) {
     }
 }
 
-// Hub distribution (between the two walker passes): a hub that holds excess
-// (the cluster aggregator collects the units the walkers bring it) hands it to
-// its admissible arcs towards no larger distance, one workgroup per
-// 1024-arc chunk claiming its share with one returning atomic (as the sweeps'
-// hub chunks do); the fed nodes are listed for the second walker pass.
-__global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
-    __shared__ long long sh[WPB];
-    __shared__ long long s_take;
+// ------------------------------------------------------- tail augmentation ---
+// A phase's tail (≤ aug_k nodes hold excess after an update): a BLOCKING FLOW over
+// the update's distances instead of one hop per sweep. Measured on the CPU
+// (tools/proto/tail_proto.c, config 3's final phase): the last ~64 units have
+// augmenting paths of (near) zero length in ε units, but long, capacity-1 and
+// competing — matching-like chains — so a blocking flow (Hopcroft–Karp style: DFS
+// with dead-end marks) routes 37 of 64 units after the first update and all of
+// them after 7, where one augmenting path per update (successive shortest
+// paths, or greedy walks without backtracking) needed ~60.
+//
+// One wave per walker. A walker runs a DFS from its source along QUALIFYING arcs:
+// residual, head not marked dead this cycle, and either admissible (rc < 0) with
+// d(w) ≤ d(u), or rc ≤ slack·ε with d(w) < d(u) (d = the update's distances; the
+// arc of least d(w) first). Advancing claims one unit of the arc's residual with a
+// CAS; a node with no qualifying arc is marked dead (cycle-stamped, shared by all
+// walkers) and the walker retreats, giving the unit back. Reaching a deficit — or
+// a hub that has no candidate list — commits the path: the reverse residuals are
+// raised, the source gives its unit, the end node takes it. Reverse residuals are
+// raised only at commit, so no walker can use a tentative path's reverse arcs.
+// ε-optimality: a unit moves along arcs of rc ≤ slack·ε, so their reverses get rc
+// ≥ −slack·ε (slack 1 in a phase that must end 1-optimal).
+// Hubs (cluster aggregator): k_hub_cands lists a hub's qualifying out-arcs once
+// per cycle (its 100k-arc segment scanned by ~100 workgroups), and walkers scan
+// that list instead; the hub's excess is split over HUB_W walkers, one unit
+// stream each.
+constexpr int DFS_PATH = 512;     // path stack (positions) per walker
+constexpr int DFS_STEPS = 4096;   // advance / retreat steps per walker and cycle
+constexpr int HC_CAP = 4096;      // candidate out-arcs listed per hub
+constexpr int HUB_W = 192;        // walkers sharing a hub's excess
+
+__device__ __forceinline__ bool walk_ok(long long rc, long long dw, long long du, long long L, long long eps,
+                                        int slack) {
+    const bool down = dw < du || du >= L;
+    return (rc < 0 && (dw <= du || du >= L)) || (rc <= slack * eps && down);
+}
+
+// Per hub chunk: a hub holding excess lists its qualifying out-arcs (non-hub heads).
+__global__ __launch_bounds__(BLK) void k_hub_cands(DG g, int slack) {
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
-    if (nx == 0 || nx > AUG_K) return;
+    if (nx == 0 || nx > g.aug_k) return;
     const HItem it = g.hitems[blockIdx.x];
     const int x = it.node;
     const long long E = atom_load(&g.excess[x]);
     if (E <= 0) return;
-    const Front F = g.sf[sseq % 3];
-    const long long eps = g.ctl->eps;
+    if (it.begin == g.first[x] && threadIdx.x == 0) g.hub_e[it.hid] = E;   // snapshot for the split
+    const long long eps = g.ctl->eps, L = g.ctl->gu_L;
     const long long dx = atom_load(&g.dist[ni(x)]);
     const long long px = g.p0[ni(x)];
-    long long r[PER_T], adm[PER_T], uc[PER_T];
-    int w[PER_T], rv[PER_T];
-    long long mine = 0;
-#pragma unroll
     for (int k = 0; k < PER_T; ++k) {
-        const int a = it.begin + threadIdx.x * PER_T + k;
-        r[k] = 0;
-        w[k] = 0;
-        rv[k] = 0;
-        uc[k] = 0;
-        adm[k] = 0;
+        const int a = it.begin + k * BLK + (int)threadIdx.x;
+        bool q = false;
         if (a < it.end) {
-            r[k] = atom_load(&g.rcap[a]);   // the first walker pass claimed with atomics
-            w[k] = g.head[a];
-            rv[k] = g.rev[a];
-            uc[k] = g.ucap[a];
+            const Pos r = ld_pos(g.pos + a);
+            if (r.rcap > 0 && r.head < g.hub_base) {
+                const long long rc = r.cost + px - g.p0[ni(r.head)];
+                q = walk_ok(rc, atom_load(&g.dist[ni(r.head)]), dx, L, eps, slack);
+            }
         }
-    }
-#pragma unroll
-    for (int k = 0; k < PER_T; ++k) {
-        const int a = it.begin + threadIdx.x * PER_T + k;
-        if (a < it.end && r[k] > 0) {
-            const long long cr = g.cost[a] + px - g.p0[ni(w[k])];
-            const long long dw = atom_load(&g.dist[ni(w[k])]);
-            if (cr <= slack * eps && (dw < dx || (dw == dx && cr < 0))) adm[k] = r[k];
-        }
-        mine += adm[k];
-    }
-    long long Ac = 0;
-    const long long excl = block_excl_scan(mine, sh, &Ac);
-    if (threadIdx.x == 0) {
-        long long take = 0;
-        if (Ac > 0) {
-            const long long start = atom_add_ret(&g.aug_req[it.hid], Ac);
-            take = E - start;
-            take = take < 0 ? 0 : (take > Ac ? Ac : take);
-        }
-        s_take = take;
-        if (take) atom_add(&g.excess[x], -take);
-    }
-    __syncthreads();
-    long long rt = s_take - excl;
-    rt = rt < 0 ? 0 : (rt > mine ? mine : rt);
-    int dummy = 0;
-#pragma unroll
-    for (int k = 0; k < PER_T; ++k) {
-        const long long d = adm[k] < rt ? adm[k] : rt;
-        rt -= d;
-        if (d <= 0) continue;
-        const int a = it.begin + threadIdx.x * PER_T + k;
-        g.rcap[a] = r[k] - d;              // only this chunk touches the pair in this kernel
-        g.rcap[rv[k]] = uc[k] - (r[k] - d);
-        const long long now = atom_add_ret(&g.excess[w[k]], d) + d;
-        if (now > 0) {
-            mark(g, F, w[k], dummy);
-            const int idx = atomicAdd(&g.ctl->n_xl2, 1);
-            if (idx < AUG_K2) g.xl2[idx] = w[k];
-        }
+        const unsigned long long m = __ballot(q);
+        if (!m) continue;
+        int base = 0;
+        if (lane_id() == 0) base = atomicAdd(&g.hub_cnt[it.hid], (int)__popcll(m));
+        base = __shfl(base, 0);
+        const int idx = base + (int)__popcll(m & ((1ULL << lane_id()) - 1));
+        if (q && idx < HC_CAP) g.hub_cand[it.hid * HC_CAP + idx] = a;
     }
 }
 
-// ------------------------------------------------------- tail augmentation ---
-// When a converged update leaves at most AUG_K nodes with excess (the tail of a
-// phase: a few units that the sweeps would move one hop per sweep over dozens
-// of update cycles — measured: ~100 cycles for the last ~50 units of a config-4
-// round), each of them sends its excess straight down the update's distances:
-// one wave per excess node walks from u along the residual arc (u, w) of least
-// distance d(w), until it reaches a deficit. An arc qualifies if d(w) < d(u)
-// (or d(w) = d(u) and it is admissible) and its reduced cost under the updated
-// prices is at most ε: the reverse arc a push creates then has reduced cost
-// ≥ −ε, so ε-optimality holds (the update's tree arcs have rc ∈ [−ε, 0); arcs
-// one length unit off the tree, rc ∈ [0, ε), let several units leave a node
-// whose tree arc carries one). Walkers claim residual capacity with a CAS
-// (they may share arcs); units that cannot go on (no arc, capacity taken, a
-// hub, the hop limit) stay where the walk stands, marked for the sweeps that
-// follow. Runs between the apply and the cycle's sweeps.
-// mode 0: from the apply's excess nodes (non-hubs); mode 1: from the nodes a hub
-// distribution (k_aug_hub) fed.
-__global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int slack) {
+// The DFS walkers: blocks [0, aug_k) start at the listed non-hub excess nodes (all
+// their units, one path each), blocks [aug_k, aug_k + HUB_W) share the excess of the
+// first hub that had some (k_hub_cands' snapshot).
+__global__ __launch_bounds__(WAVE) void k_dfs_walk(DG g, int sseq, int slack, int stamp) {
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
-    if (nx == 0 || nx > AUG_K) return;
-    const int cnt = mode ? min(g.ctl->n_xl2, AUG_K2) : nx;
-    if ((int)blockIdx.x >= cnt) return;
+    if (nx == 0 || nx > g.aug_k) return;
+    __shared__ int path[DFS_PATH];
     const int lane = lane_id();
     const Front F = g.sf[sseq % 3];
-    const long long eps = g.ctl->eps;
-    int u = mode ? g.xl2[blockIdx.x] : g.xl[blockIdx.x];
-    if (u < 0 || u >= g.hub_base) return;   // hubs: k_aug_hub
-    long long carry = 0;
-    if (lane == 0) carry = atom_exch(&g.excess[u], 0LL);
-    carry = __shfl(carry, 0);
-    if (carry <= 0) {
-        if (lane == 0 && carry < 0) atom_add(&g.excess[u], carry);   // (not an excess node any more)
-        return;
-    }
-    long long du = atom_load(&g.dist[ni(u)]);
-    long long pu = g.p0[ni(u)];
-    int hops = 0, reached = 0, dummy = 0;
-    for (int step = 0; step < AUG_STEPS; ++step) {
-        int b0, en;
-        seg_of(g.p0, u, b0, en);
-        // the qualifying residual arc (rc ≤ slack·ε; d(w) < d(u), or d(w) = d(u) and
-        // rc < 0) of least d(w) (ties: lowest position)
-        long long bd = INF64;
-        int ba = -1;
-        for (int base = b0; base < en; base += WAVE) {
-            const int a = base + lane;
-            long long key = INF64;
-            if (a < en) {
-                const long long r = atom_load(&g.rcap[a]);   // other walkers claim with atomics
-                const int w = g.head[a];
-                const long long cr = g.cost[a] + pu - g.p0[ni(w)];
-                const long long dw = atom_load(&g.dist[ni(w)]);
-                if (r > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
+    const long long eps = g.ctl->eps, L = g.ctl->gu_L;
+    int s = -1, hs = -1;          // source node; its hub index when it is a hub
+    long long units = 0;
+    if ((int)blockIdx.x < g.aug_k) {
+        if ((int)blockIdx.x >= nx) return;
+        s = g.xl[blockIdx.x];
+        if (s < 0 || s >= g.hub_base) return;
+        units = atom_load(&g.excess[s]);
+    } else {
+        const int k = (int)blockIdx.x - g.aug_k;
+        for (int h = 0; h < g.nheavy && h < HUB_LDS; ++h) {
+            const long long E = atom_load(&g.hub_e[h]);
+            if (E <= 0 || atom_load_i(&g.hub_cnt[h]) <= 0) continue;
+            const long long nw = E < HUB_W ? E : HUB_W;
+            if (k < nw) {
+                s = g.hub_base + h;
+                hs = h;
+                units = E / nw + (k < E % nw ? 1 : 0);
             }
-            const long long mn = wave_min(key);
-            if (mn < bd) {
-                const unsigned long long hit = __ballot(key == mn);
-                bd = mn;
-                ba = base + __ffsll((long long)hit) - 1;
-            }
-        }
-        if (ba < 0) break;
-        // claim min(carry, residual) on arc ba
-        long long take = 0;
-        int w = 0;
-        if (lane == 0) {
-            w = g.head[ba];
-            long long r = atom_load(&g.rcap[ba]);
-            for (;;) {
-                take = r < carry ? r : carry;
-                if (take <= 0) {
-                    take = 0;
-                    break;
-                }
-                long long exp = r;
-                if (__hip_atomic_compare_exchange_strong(&g.rcap[ba], &exp, r - take, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    break;
-                r = exp;
-            }
-            if (take > 0) atom_add(&g.rcap[g.rev[ba]], take);
-            if (take < carry) {   // the rest stays at u
-                atom_add(&g.excess[u], carry - take);
-                mark(g, F, u, dummy);
-            }
-        }
-        take = __shfl(take, 0);
-        w = __shfl(w, 0);
-        if (take == 0) {
-            carry = 0;   // deposited at u above
             break;
         }
-        carry = take;
-        ++hops;
-        u = w;
-        du = bd;
-        if (lane == 0) {
-            const long long e = atom_load(&g.excess[u]);
-            if (e < 0 || u >= g.hub_base) {   // a deficit (or a hub: the sweeps take over)
-                const long long now = atom_add_ret(&g.excess[u], carry) + carry;
-                if (now > 0) mark(g, F, u, dummy);
-                reached = e < 0 ? 1 : 0;
-                carry = 0;
+        if (s < 0) return;
+    }
+    int dummy = 0, reached = 0, steps = 0, hops = 0;
+    long long left = units;
+    while (left > 0 && steps < DFS_STEPS) {
+        // one DFS from s for one unit
+        int plen = 0, u = s, t = -1;
+        bool fail = false;
+        while (steps < DFS_STEPS) {
+            ++steps;
+            const bool uhub = u >= g.hub_base;
+            const int uh = u - g.hub_base;
+            if (u != s) {
+                const long long eu = atom_load(&g.excess[u]);
+                const bool no_list =
+                    uhub && (uh >= HUB_LDS || atom_load(&g.hub_e[uh]) <= 0 || atom_load_i(&g.hub_cnt[uh]) <= 0);
+                if (eu < 0 || no_list) {   // a deficit, or a hub without a candidate list: deposit there
+                    t = u;
+                    break;
+                }
             }
+            const long long du = atom_load(&g.dist[ni(u)]);
+            const long long pu = g.p0[ni(u)];
+            // the qualifying arc of least d(w) (ties: lowest index)
+            long long bd = INF64;
+            int ba = -1;
+            int lo, hi;
+            const int* cand = nullptr;
+            if (uhub) {
+                cand = g.hub_cand + uh * HC_CAP;
+                lo = 0;
+                hi = min(atom_load_i(&g.hub_cnt[uh]), HC_CAP);
+            } else {
+                seg_of(g.p0, u, lo, hi);
+            }
+            // hub walkers spread over the list: each starts its scan at its own chunk
+            const int n_it = (hi - lo + WAVE - 1) / WAVE;
+            const int rot = uhub ? (int)blockIdx.x % max(1, n_it) : 0;
+            for (int it = 0; it < n_it; ++it) {
+                const int i = lo + ((it + rot) % n_it) * WAVE + lane;
+                long long key = INF64;
+                int a = -1;
+                if (i < hi) {
+                    a = cand ? cand[i] : i;
+                    const Pos r = ld_pos(g.pos + a);
+                    const long long rr = atom_load(&g.pos[a].rcap);   // claims by other walkers
+                    const int w = r.head;
+                    if (rr > 0 && w != u && g.dead[w] != stamp) {
+                        const long long dw = atom_load(&g.dist[ni(w)]);
+                        if (walk_ok(r.cost + pu - g.p0[ni(w)], dw, du, L, eps, slack)) key = dw;
+                    }
+                }
+                const long long mn = wave_min(key);
+                if (mn < bd) {
+                    const unsigned long long hit = __ballot(key == mn);
+                    bd = mn;
+                    ba = __shfl(a, __ffsll((long long)hit) - 1);
+                }
+                if (uhub && bd < INF64) break;   // at a hub the first chunk with a candidate will do
+            }
+            bool adv = false;
+            if (ba >= 0 && plen < DFS_PATH) {
+                int ok = 0;
+                if (lane == 0) {   // claim one unit of the arc
+                    long long r = atom_load(&g.pos[ba].rcap);
+                    while (r > 0) {
+                        long long exp = r;
+                        if (__hip_atomic_compare_exchange_strong(&g.pos[ba].rcap, &exp, r - 1, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            ok = 1;
+                            break;
+                        }
+                        r = exp;
+                    }
+                }
+                adv = __shfl(ok, 0) != 0;
+                if (!adv) continue;   // lost the race for it: scan u again
+            }
+            if (adv) {
+                if (lane == 0) path[plen] = ba;
+                __syncthreads();
+                ++plen;
+                u = g.pos[ba].head;
+                continue;
+            }
+            // no qualifying arc: u is a dead end this cycle
+            if (lane == 0) g.dead[u] = stamp;
+            if (plen == 0) {
+                fail = true;   // the source itself: its units stay
+                break;
+            }
+            const int a = path[--plen];
+            if (lane == 0) atom_add(&g.pos[a].rcap, 1LL);   // give the unit back
+            u = g.pos[g.pos[a].rev].head;
         }
-        carry = __shfl(carry, 0);
-        if (carry == 0) break;
-        pu = g.p0[ni(u)];
+        if (t < 0) {   // no path (or out of steps): release what the DFS still holds
+            for (int i = lane; i < plen; i += WAVE) atom_add(&g.pos[path[i]].rcap, 1LL);
+            fail = true;
+        } else {       // commit: reverse residuals, the unit from s to t
+            for (int i = lane; i < plen; i += WAVE) atom_add(&g.pos[g.pos[path[i]].rev].rcap, 1LL);
+            if (lane == 0) {
+                atom_add(&g.excess[s], -1LL);
+                const long long now = atom_add_ret(&g.excess[t], 1LL) + 1;
+                if (now > 0) mark(g, F, t, dummy);   // overfilled deficit / hub deposit: the sweeps take it
+            }
+            hops += plen;
+            reached += t >= 0 && atom_load(&g.excess[t]) <= 0;
+            --left;
+        }
+        __syncthreads();
+        if (fail) break;
     }
     if (lane == 0) {
-        if (carry > 0) {   // hop limit or no admissible arc: the units stay at u
-            atom_add(&g.excess[u], carry);
-            mark(g, F, u, dummy);
-        }
+        if (left > 0) mark(g, F, s, dummy);   // the units that found no path stay (sweeps)
         const int sh = (int)blockIdx.x & (CTR_SHARDS - 1);
-        atomicAdd(reached ? &g.ctl->aug_reached : &g.ctl->aug_short, 1);
-        if (reached) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, 1ULL);
+        atomicAdd(units - left > 0 ? &g.ctl->aug_reached : &g.ctl->aug_short, 1);
+        if (units - left > 0) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, (unsigned long long)(units - left));
         if (hops) atomicAdd(g.ctr + sh * NCTR + C_AUGHOP, (unsigned long long)hops);
     }
+    (void)hs;
+    (void)reached;
 }
 
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
@@ -2064,7 +2210,7 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
             continue;
         }
         const long long cp = cap[i] - low[i];
-        const long long rf = g.rcap[p], rr = g.rcap[g.rev[p]];
+        const long long rf = g.pos[p].rcap, rr = g.pos[g.pos[p].rev].rcap;
         const long long f = cp - rf;
         if (rf < 0 || rr < 0 || f < 0 || f != rr) bad = 1;
         const long long fl = f + low[i];
@@ -2086,9 +2232,9 @@ __global__ void k_verify_opt(DG g, long long m2) {
     int bad = 0;
     const long long eps = g.ctl->eps;
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
-        if (g.rcap[p] > 0) {
-            const int t = g.head[g.rev[p]];
-            const long long cr = g.cost[p] + g.p0[ni(t)] - g.p0[ni(g.head[p])];
+        if (g.pos[p].rcap > 0) {
+            const int t = g.pos[g.pos[p].rev].head;
+            const long long cr = g.pos[p].cost + g.p0[ni(t)] - g.p0[ni(g.pos[p].head)];
             if (cr < -eps) bad = 1;
         }
     }
@@ -2108,19 +2254,18 @@ __global__ void k_verify_nodes(DG g) {
 // state consistent with every delta). Across a rebuild they are carried by arc
 // slot and node slot: saved before, restored (clamped to the new bounds) after.
 __global__ void k_save_flows(int hi, const unsigned char* __restrict__ alive, const int* __restrict__ fwd,
-                             const int* __restrict__ rev, const long long* __restrict__ rcap,
-                             long long* __restrict__ saved) {
+                             const Pos* __restrict__ pos, long long* __restrict__ saved) {
     for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
         const int p = fwd[s];
-        saved[s] = (alive[s] && p >= 0) ? rcap[rev[p]] : 0;
+        saved[s] = (alive[s] && p >= 0) ? pos[pos[p].rev].rcap : 0;
     }
 }
 
 __global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive, const long long* __restrict__ saved,
                                 const long long* __restrict__ low, const long long* __restrict__ cap,
-                                const int* __restrict__ fwd, const int* __restrict__ rev,
-                                const int* __restrict__ src, const int* __restrict__ dst, const int* __restrict__ perm,
-                                long long* __restrict__ rcap, long long* __restrict__ excess) {
+                                const int* __restrict__ fwd, const int* __restrict__ src,
+                                const int* __restrict__ dst, const int* __restrict__ perm, Pos* __restrict__ pos,
+                                long long* __restrict__ excess) {
     for (long long s = blockIdx.x * (long long)BLK + threadIdx.x; s < hi; s += (long long)gridDim.x * BLK) {
         if (!alive[s]) continue;
         const long long u = cap[s] - low[s];
@@ -2128,8 +2273,8 @@ __global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive,
         f = f < 0 ? 0 : (f > u ? u : f);
         if (f > 0) {
             const int p = fwd[s];
-            rcap[p] = u - f;
-            rcap[rev[p]] = f;
+            pos[p].rcap = u - f;
+            pos[pos[p].rev].rcap = f;
             atom_add(&excess[perm[src[s]]], -f);
             atom_add(&excess[perm[dst[s]]], f);
         }
@@ -2165,7 +2310,7 @@ __global__ void k_fresh_prices(int ncap, const unsigned char* __restrict__ fresh
         const int x = perm[v];
         long long best = -INF64;
         for (int a = g.first[x]; a < g.first[x + 1]; ++a)
-            if (g.rcap[a] > 0) best = max(best, g.p0[ni(g.head[a])] - g.cost[a]);
+            if (g.pos[a].rcap > 0) best = max(best, g.p0[ni(g.pos[a].head)] - g.pos[a].cost);
         if (best > -INF64) {
             g.p0[ni(x)] = best;
             g.p1[ni(x)] = best;
@@ -2177,8 +2322,8 @@ __global__ void k_fresh_prices(int ncap, const unsigned char* __restrict__ fresh
 __global__ void k_max_viol(DG g, long long m2) {
     long long mx = 0;
     for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
-        if (g.rcap[p] > 0) {
-            const long long cr = g.cost[p] + g.p0[ni(g.head[g.rev[p]])] - g.p0[ni(g.head[p])];
+        if (g.pos[p].rcap > 0) {
+            const long long cr = g.pos[p].cost + g.p0[ni(g.pos[g.pos[p].rev].head)] - g.p0[ni(g.pos[p].head)];
             if (-cr > mx) mx = -cr;
         }
     }
@@ -2226,7 +2371,7 @@ __device__ __forceinline__ int find_unit(const long long* __restrict__ scan, con
 }
 
 __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, const int* __restrict__ first,
-                             const int* __restrict__ head, const int* __restrict__ rev,
+                             const Pos* __restrict__ pos,
                              const long long* __restrict__ outv, const long long* __restrict__ outs,
                              const long long* __restrict__ inv, const long long* __restrict__ ins,
                              const int* __restrict__ iperm, const unsigned char* __restrict__ itype,
@@ -2245,9 +2390,9 @@ __global__ void k_task_paths(int ncap, int nn, const int* __restrict__ perm, con
             if (k >= otot) break;   // absorbed here (no outflow left)
             const int p = find_unit(outs, outv, lo, hi, obase, k);
             const long long off = k - (outs[p] - obase);
-            const int y = head[p];
+            const int y = pos[p].head;
             if (itype[y] == KS_NODE_PU) last_pu = y;
-            const int q = rev[p];
+            const int q = pos[p].rev;
             k = ins[q] - ins[first[y]] + off;
             x = y;
         }
@@ -2415,8 +2560,9 @@ struct EngineImpl {
     int64_t ncap = 0;         // node slots covered by the build
     long long mult = 1;       // cost multiplier (ncap + 1)
     int64_t m2cap = 0;        // residual positions (Σ segment capacities)
-    DBuf<int> first, head, rev, ent, used, perm, iperm;
-    DBuf<long long> rcap, ucap, scost, excess;
+    DBuf<int> first, ent, used, scur, perm, iperm;
+    DBuf<Pos> pos;
+    DBuf<long long> excess;
     DBuf<long long> nd;            // node records [p0, dist, p1, pad] × nn
     DBuf<unsigned> keys_in, keys_out;
     DBuf<int> vals_in, vals_out, pos_of, deg, capv, capi, rs;
@@ -2431,8 +2577,10 @@ struct EngineImpl {
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
-    DBuf<int> xl, xl2;                 // walker start nodes (k_augment)
-    DBuf<long long> aug_req;           // per hub claim counter (k_aug_hub)
+    DBuf<int> xl;                      // walker start nodes (k_dfs_walk)
+    DBuf<int> dead, hub_cand, hub_cnt; // walkers: dead-end stamps, hub candidate lists
+    DBuf<long long> hub_e;
+    int walk_stamp = 0;                // per cycle (dead-end marks)
     DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;        // pinned host mirror
@@ -2474,10 +2622,8 @@ struct EngineImpl {
         d.a_cost = a_cost.p;
         d.fwd = fwd.p;
         d.first = first.p;
-        d.head = head.p;
-        d.rev = rev.p;
+        d.pos = pos.p;
         d.ent = ent.p;
-        d.scost = scost.p;
         d.mult = mult;
         d.csr_valid = csr_valid ? 1 : 0;
         return d;
@@ -2494,14 +2640,14 @@ struct EngineImpl {
         a_src.release(); a_dst.release(); fwd.release(); free_stack.release(); a_low.release(); a_cap.release();
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
-        first.release(); head.release(); rev.release(); ent.release(); used.release(); perm.release(); iperm.release();
-        rcap.release(); ucap.release(); scost.release(); excess.release(); nd.release();
+        first.release(); pos.release(); ent.release(); used.release(); scur.release(); perm.release(); iperm.release();
+        excess.release(); nd.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
         q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
-        flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
+        flags.release(); hubflags.release(); ctr.release(); xl.release(); dead.release(); hub_cand.release(); hub_cnt.release(); hub_e.release(); ctl.release(); saved_flows.release(); p_slot.release();
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
@@ -2551,12 +2697,9 @@ struct EngineImpl {
         d.nn = nn;
         d.first = first.p;
         d.used = used.p;
-        d.head = head.p;
-        d.rev = rev.p;
+        d.scur = scur.p;
+        d.pos = pos.p;
         d.ent = ent.p;
-        d.rcap = rcap.p;
-        d.ucap = ucap.p;
-        d.scost = scost.p;
         d.excess = excess.p;
         d.mult = mult;
         d.csr_valid = csr_valid ? 1 : 0;
@@ -2570,11 +2713,7 @@ struct EngineImpl {
         g.m = 0;
         g.hub_base = hub_base;
         g.first = first.p;
-        g.head = head.p;
-        g.rev = rev.p;
-        g.rcap = rcap.p;
-        g.ucap = ucap.p;
-        g.cost = scost.p;
+        g.pos = pos.p;
         g.excess = excess.p;
         g.p0 = nd.p;
         g.p1 = nd.p ? nd.p + 2 : nullptr;
@@ -2594,8 +2733,10 @@ struct EngineImpl {
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
         g.xl = xl.p;
-        g.xl2 = xl2.p;
-        g.aug_req = aug_req.p;
+        g.dead = dead.p;
+        g.hub_cand = hub_cand.p;
+        g.hub_cnt = hub_cnt.p;
+        g.hub_e = hub_e.p;
         g.q_req = q_req.p;
         g.q_taken = q_taken.p;
         g.q_min = q_min.p;
@@ -2665,8 +2806,7 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     }
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
-    KS_CHECK(s.xl.ensure(AUG_K));
-    KS_CHECK(s.xl2.ensure(AUG_K2));
+    KS_CHECK(s.xl.ensure(AUG_KMAX));
     KS_CHECK(s.sctl.ensure(1));
     KS_CHECK(hipMemset(s.sctl.p, 0, sizeof(StoreCtl)));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
@@ -2927,6 +3067,8 @@ static int build(EngineImpl& s, std::string& err) {
     KS_CHECK(s.iperm.ensure(nn + 1));
     KS_CHECK(s.first.ensure(nn + 1));
     KS_CHECK(s.used.ensure(std::max(nn, 1)));
+    KS_CHECK(s.scur.ensure(std::max(nn, 1)));
+    KS_CHECK(hipMemsetAsync(s.scur.p, 0, std::max(nn, 1) * sizeof(int), st));
     KS_CHECK(s.rs.ensure(nn + 1));
     KS_CHECK(hipMemsetAsync(s.capi.p, 0, (nn + 1) * sizeof(int), st));
     KS_CHECK(hipMemsetAsync(s.iperm.p, 0xff, (nn + 1) * sizeof(int), st));
@@ -2944,19 +3086,15 @@ static int build(EngineImpl& s, std::string& err) {
     KS_CHECK(hipStreamSynchronize(st));
     s.m2cap = m2c;
     const int64_t m2cap = std::max<int64_t>(m2c, 1);
-    KS_CHECK(s.head.ensure(m2cap));
-    KS_CHECK(s.rev.ensure(m2cap));
+    KS_CHECK(s.pos.ensure(m2cap));
     KS_CHECK(s.ent.ensure(m2cap));
-    KS_CHECK(s.rcap.ensure(m2cap));
-    KS_CHECK(s.ucap.ensure(m2cap));
-    KS_CHECK(s.scost.ensure(m2cap));
     KS_CHECK(s.excess.ensure(std::max(nn, 1)));
     KS_CHECK(s.nd.ensure(4 * (size_t)std::max(nn, 1)));
     if (nn)
         hipLaunchKernelGGL(k_node_bounds, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, (const int*)s.first.p, s.nd.p);
     if (m2c)
         hipLaunchKernelGGL(k_inert_all, dim3(grid_for(m2c)), dim3(BLK), 0, st, (long long)m2c, nn,
-                           (const int*)s.first.p, s.head.p, s.rev.p, s.ent.p, s.rcap.p, s.ucap.p, s.scost.p);
+                           (const int*)s.first.p, s.pos.p, s.ent.p);
     // 3. live arcs into their segments, ordered by tail (radix sort of 2·hi keys)
     const int64_t m2 = 2 * (int64_t)hi;
     if (s.acap) KS_CHECK(hipMemsetAsync(s.fwd.p, 0xff, s.acap * sizeof(int), st));
@@ -2984,9 +3122,9 @@ static int build(EngineImpl& s, std::string& err) {
                            (const unsigned*)s.keys_out.p, (const int*)s.vals_out.p, (const int*)s.rs.p,
                            (const int*)s.first.p, (const int*)s.perm.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
                            (const long long*)s.a_low.p, (const long long*)s.a_cap.p, (const long long*)s.a_cost.p,
-                           s.mult, s.head.p, s.rcap.p, s.ucap.p, s.scost.p, s.ent.p, s.fwd.p, s.pos_of.p);
+                           s.mult, s.pos.p, s.ent.p, s.fwd.p, s.pos_of.p);
         hipLaunchKernelGGL(k_fill_rev, dim3(grid_for(m2)), dim3(BLK), 0, st, (long long)m2, nn,
-                           (const unsigned*)s.keys_out.p, (const int*)s.vals_out.p, (const int*)s.pos_of.p, s.rev.p);
+                           (const unsigned*)s.keys_out.p, (const int*)s.vals_out.p, (const int*)s.pos_of.p, s.pos.p);
         hipLaunchKernelGGL(k_used, dim3(grid_for(nn)), dim3(BLK), 0, st, nn, (const int*)s.rs.p, s.used.p);
     } else {
         KS_CHECK(hipMemsetAsync(s.used.p, 0, std::max(nn, 1) * sizeof(int), st));
@@ -3034,7 +3172,14 @@ static int build(EngineImpl& s, std::string& err) {
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
         const int nq = std::max(1, s.nheavy);
         KS_CHECK(s.q_req.ensure(nq));
-        KS_CHECK(s.aug_req.ensure(nq));
+        KS_CHECK(s.hub_cand.ensure((size_t)nq * HC_CAP));
+        KS_CHECK(s.hub_cnt.ensure(nq));
+        KS_CHECK(s.hub_e.ensure(nq));
+        KS_CHECK(hipMemsetAsync(s.hub_cnt.p, 0, nq * sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(s.hub_e.p, 0, nq * sizeof(long long), st));
+        KS_CHECK(s.dead.ensure(std::max(1, s.nn)));
+        KS_CHECK(hipMemsetAsync(s.dead.p, 0, std::max(1, s.nn) * sizeof(int), st));
+        s.walk_stamp = 0;
         KS_CHECK(s.q_taken.ensure(nq));
         KS_CHECK(s.q_min.ensure(nq));
         KS_CHECK(s.q_unsat.ensure(nq));
@@ -3058,7 +3203,7 @@ static int cold_reset(EngineImpl& s, std::string& err) {
     const int hi = s.hi();
     if (s.m2cap)
         hipLaunchKernelGGL(k_reset_pos, dim3(grid_for(s.m2cap)), dim3(BLK), 0, st, (long long)s.m2cap,
-                           (const int*)s.ent.p, (const long long*)s.ucap.p, s.rcap.p);
+                           (const int*)s.ent.p, s.pos.p);
     hipLaunchKernelGGL(k_reset_nodes, dim3(grid_for(s.nn)), dim3(BLK), 0, st, s.nn, (int)s.ncap,
                        (const int*)s.iperm.p, (const unsigned char*)s.n_alive.p, (const long long*)s.n_supply.p,
                        s.excess.p, s.nd.p, (s.nd.p + 2));
@@ -3121,7 +3266,7 @@ int Engine::task_pu(uint64_t* dev_out, size_t cap, size_t* count, int64_t n_task
     tt = s.map_tmp.n;
     KS_CHECK(hipcub::DeviceScan::ExclusiveSum(s.map_tmp.p, tt, s.map_is_task.p, s.map_rank.p, (int)ncap, st));
     hipLaunchKernelGGL(k_task_paths, dim3(grid_for(ncap)), dim3(BLK), 0, st, (int)ncap, nn, (const int*)s.perm.p,
-                       (const int*)s.first.p, (const int*)s.head.p, (const int*)s.rev.p,
+                       (const int*)s.first.p, (const Pos*)s.pos.p,
                        (const long long*)s.map_outv.p, (const long long*)s.map_outs.p,
                        (const long long*)s.map_inv.p, (const long long*)s.map_ins.p, (const int*)s.iperm.p,
                        (const unsigned char*)s.map_itype.p, (const int*)s.map_rank.p,
@@ -3457,8 +3602,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_CHECK(s.p_slot.ensure(std::max<int64_t>(ncap_prev, 1)));
             if (hi0)
                 hipLaunchKernelGGL(k_save_flows, dim3(grid_for(hi0)), dim3(BLK), 0, st, hi0,
-                                   (const unsigned char*)s.a_alive.p, (const int*)s.fwd.p, (const int*)s.rev.p,
-                                   (const long long*)s.rcap.p, s.saved_flows.p);
+                                   (const unsigned char*)s.a_alive.p, (const int*)s.fwd.p, (const Pos*)s.pos.p,
+                                   s.saved_flows.p);
             hipLaunchKernelGGL(k_save_prices, dim3(grid_for(ncap_prev)), dim3(BLK), 0, st, (int)ncap_prev,
                                (const int*)s.perm.p, (const long long*)s.nd.p, s.p_slot.p);
         }
@@ -3471,8 +3616,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 hipLaunchKernelGGL(k_restore_flows, dim3(grid_for(hi0)), dim3(BLK), 0, st, hi0,
                                    (const unsigned char*)s.a_alive.p, (const long long*)s.saved_flows.p,
                                    (const long long*)s.a_low.p, (const long long*)s.a_cap.p, (const int*)s.fwd.p,
-                                   (const int*)s.rev.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
-                                   (const int*)s.perm.p, s.rcap.p, s.excess.p);
+                                   (const int*)s.a_src.p, (const int*)s.a_dst.p, (const int*)s.perm.p, s.pos.p,
+                                   s.excess.p);
             hipLaunchKernelGGL(k_restore_prices, dim3(grid_for(s.ncap)), dim3(BLK), 0, st, (int)s.ncap,
                                (int)ncap_prev, mult_prev, s.mult, (const long long*)s.p_slot.p, (const int*)s.perm.p,
                                s.nd.p, (s.nd.p + 2));
@@ -3524,6 +3669,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const ks_opts& o = s.opts;
     DG g = s.dg();
     g.expand = o.two_hop < 0 ? 0 : 1;      // two hops per round through tasks and PUs
+    g.aug_k = o.tail_nodes > 0 ? std::min(AUG_KMAX, (int)o.tail_nodes) : 64;
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
     const int sgrid = s.sparse_grid();     // sparse Bellman-Ford rounds
@@ -3539,6 +3685,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int nhit = s.nhitems;
     const bool use_aug = o.walk_slack >= 0;               // tail augmentation (walks)
     const int aug_slack = o.walk_slack > 0 ? o.walk_slack : 4;   // walks take arcs of rc <= slack·ε
+    const int walk_passes = o.walk_passes > 0 ? std::min(8, (int)o.walk_passes) : 1;
     // Bellman-Ford rounds enqueued per cycle: the last update's count + kb_margin,
     // at least kb_min (a launch that finds the update converged still costs ≈ 5 µs
     // with the gap before the next kernel; an update that needs more than was
@@ -3656,10 +3803,16 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
-            if (use_aug) {   // tail augmentation: walkers, hub distribution, walkers from what it fed
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
-                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, walk_sl);
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, walk_sl);
+            if (use_aug) {   // tail: a blocking flow over the update's distances (DFS walkers)
+                if (nhit) hipLaunchKernelGGL(k_hub_cands, dim3(nhit), dim3(BLK), 0, st, g, walk_sl);
+                for (int wp = 0; wp < walk_passes; ++wp) {
+                    if (++s.walk_stamp >= (1 << 30)) {   // (never in practice) restart the stamps
+                        s.walk_stamp = 1;
+                        (void)hipMemsetAsync(s.dead.p, 0, std::max(1, nn) * sizeof(int), st);
+                    }
+                    hipLaunchKernelGGL(k_dfs_walk, dim3(g.aug_k + HUB_W), dim3(WAVE), 0, st, g, sseq, walk_sl,
+                                       s.walk_stamp);
+                }
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
@@ -3723,7 +3876,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
-            gi = (use_aug && hc->n_exc <= AUG_K) ? gi_tail : gi_base;
+            gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +

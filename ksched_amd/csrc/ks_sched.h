@@ -7,6 +7,7 @@
 #include <cstdint>
 
 #include "../../include/ksmcmf.h"
+#include "ks_pos.h"
 
 namespace ks {
 
@@ -27,10 +28,8 @@ struct SchedDev {
     long long* a_cost;
     const int* fwd;
     const int* first;              // residual CSR (internal ids)
-    const int* head;
-    const int* rev;
+    Pos* pos;                      // residual positions (ks_pos.h)
     const int* ent;
-    long long* scost;
     long long mult;
     int csr_valid;
 };

@@ -97,7 +97,7 @@ __global__ void k_topo_level(SchedDev d, const int* __restrict__ front, int nfro
         for (int p = d.first[x] + lane; p < d.first[x + 1]; p += 64) {
             const int e = d.ent[p];
             if (e < 0 || !(e & 1)) continue;    // live in-arcs only (reverse positions)
-            const int u = d.head[p];
+            const int u = d.pos[p].head;
             const int us = d.iperm[u];
             if (atomicCAS(&lvl[u], -1, level + 1) == -1) next[atomicAdd(nnext, 1)] = u;
             const unsigned char tu = d.n_type[us];
@@ -159,8 +159,8 @@ __device__ __forceinline__ void set_cost(const SchedDev& d, int s, long long c, 
     d.a_cost[s] = c;
     const int p = d.fwd[s];
     if (d.csr_valid && p >= 0) {
-        d.scost[p] = c * d.mult;
-        d.scost[d.rev[p]] = -c * d.mult;
+        d.pos[p].cost = c * d.mult;
+        d.pos[d.pos[p].rev].cost = -c * d.mult;
     }
     atomicAdd(changed, 1);
 }

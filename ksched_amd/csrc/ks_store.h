@@ -20,6 +20,7 @@
 #include <cstdint>
 
 #include "../../include/ksmcmf.h"
+#include "ks_pos.h"
 
 namespace ks {
 
@@ -84,12 +85,9 @@ struct StoreDev {
     int nn;
     const int* first;             // segment starts, first[v + 1] − first[v] = capacity
     int* used;                    // positions handed out in each segment
-    int* head;
-    int* rev;
+    int* scur;                    // per node: chunk cursor of the inert-position scan
+    Pos* pos;                     // residual positions (ks_pos.h)
     int* ent;                     // position → 2·slot + (reverse ? 1 : 0), −1 = dead
-    long long* rcap;
-    long long* ucap;
-    long long* scost;
     long long* excess;
     long long mult;               // cost multiplier (node capacity + 1)
     int csr_valid;                // 0: table-only apply (a rebuild follows)

@@ -74,11 +74,11 @@ __device__ __forceinline__ void h_tomb(const StoreDev& d, int e) {
 
 __device__ __forceinline__ void inert(const StoreDev& d, int p, int owner) {
     d.ent[p] = -1;
-    d.rcap[p] = 0;
-    d.ucap[p] = 0;
-    d.scost[p] = DEAD_COST;
-    d.head[p] = owner;
-    d.rev[p] = p;
+    d.pos[p].rcap = 0;
+    d.pos[p].ucap = 0;
+    d.pos[p].cost = DEAD_COST;
+    d.pos[p].head = owner;
+    d.pos[p].rev = p;
 }
 
 __device__ __forceinline__ int perm_of(const StoreDev& d, int slot) { return slot < d.ncap ? d.perm[slot] : -1; }
@@ -90,8 +90,8 @@ __device__ void kill_positions(const StoreDev& d, int s) {
     const int p = d.fwd[s];
     if (p < 0) return;
     d.fwd[s] = -1;
-    const int q = d.rev[p];
-    const long long f = d.rcap[q] + d.a_low[s];
+    const int q = d.pos[p].rev;
+    const long long f = d.pos[q].rcap + d.a_low[s];
     const int xs = perm_of(d, d.a_src[s]), xd = perm_of(d, d.a_dst[s]);
     if (f) {
         atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)f);
@@ -108,6 +108,30 @@ __device__ __forceinline__ void free_slot(const StoreDev& d, int s) {
     d.free_stack[t] = s;
     atomicSub(&d.ctl->live, 1);
     atomicAdd(&d.ctl->killed, 1);
+}
+
+// A free (inert, ent = −1) position in node x's segment, claimed for the entry
+// tag with a CAS on ent, or −1 when the segment has none. First the next never
+// used position (the fill counter), then — once the segment has been filled —
+// the positions that removed arcs left inert, found by scanning 64-position
+// chunks from a per-node cursor (inserts and removals balance in a churning
+// cell, so hubs such as the cluster aggregator and the sink keep their slack
+// instead of forcing a CSR rebuild every few rounds).
+__device__ int claim_pos(const StoreDev& d, int x, int tag) {
+    const int b = d.first[x], e = d.first[x + 1], cap = e - b;
+    const int ps = atomicAdd(&d.used[x], 1);
+    if (ps < cap && atomicCAS(&d.ent[b + ps], -1, tag) == -1) return b + ps;
+    constexpr int SCAN = 64;
+    const int chunks = (cap + SCAN - 1) / SCAN;
+    for (int k = 0; k < chunks && k < 64; ++k) {
+        const int c = (int)((unsigned)atomicAdd(&d.scur[x], 1) % (unsigned)chunks);
+        const int lo = b + c * SCAN, hi = min(e, lo + SCAN);
+        for (int p = lo; p < hi; ++p)
+            if (__hip_atomic_load(&d.ent[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1 &&
+                atomicCAS(&d.ent[p], -1, tag) == -1)
+                return p;
+    }
+    return -1;
 }
 
 __device__ __forceinline__ bool is_arc_record(const ks_delta& x) {
@@ -245,15 +269,15 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
         }
         const int p0 = d.fwd[s];
         if (p0 >= 0) {                  // in place: same endpoints, new bounds / cost
-            const int q0 = d.rev[p0];
-            const long long f = d.rcap[q0];
+            const int q0 = d.pos[p0].rev;
+            const long long f = d.pos[q0].rcap;
             const long long fn = f < 0 ? 0 : (f > u ? u : f);
-            d.rcap[p0] = u - fn;
-            d.rcap[q0] = fn;
-            d.ucap[p0] = u;
-            d.ucap[q0] = u;
-            d.scost[p0] = x.cost * d.mult;
-            d.scost[q0] = -x.cost * d.mult;
+            d.pos[p0].rcap = u - fn;
+            d.pos[q0].rcap = fn;
+            d.pos[p0].ucap = u;
+            d.pos[q0].ucap = u;
+            d.pos[p0].cost = x.cost * d.mult;
+            d.pos[q0].cost = -x.cost * d.mult;
             const long long back = (f - fn) - (low - low_old);   // units returned to the tail
             if (back) {
                 atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)back);
@@ -262,25 +286,24 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
             atomicAdd(&d.ctl->updated, 1);
             continue;
         }
-        const int ps = atomicAdd(&d.used[xs], 1), pd = atomicAdd(&d.used[xd], 1);
-        const int p = d.first[xs] + ps, q = d.first[xd] + pd;
-        if (p >= d.first[xs + 1] || q >= d.first[xd + 1]) {
+        const int p = claim_pos(d, xs, 2 * s), q = p < 0 ? -1 : claim_pos(d, xd, 2 * s + 1);
+        if (p < 0 || q < 0) {
             d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
-            if (p >= d.first[xs + 1]) d.n_grow[sl] = 1;
-            if (q >= d.first[xd + 1]) d.n_grow[dl] = 1;
+            if (p < 0) d.n_grow[sl] = 1;
+            else d.n_grow[dl] = 1;
             continue;
         }
-        d.head[p] = xd;
-        d.rev[p] = q;
-        d.rcap[p] = u;
-        d.ucap[p] = u;
-        d.scost[p] = x.cost * d.mult;
+        d.pos[p].head = xd;
+        d.pos[p].rev = q;
+        d.pos[p].rcap = u;
+        d.pos[p].ucap = u;
+        d.pos[p].cost = x.cost * d.mult;
         d.ent[p] = 2 * s;
-        d.head[q] = xs;
-        d.rev[q] = p;
-        d.rcap[q] = 0;
-        d.ucap[q] = u;
-        d.scost[q] = -x.cost * d.mult;
+        d.pos[q].head = xs;
+        d.pos[q].rev = p;
+        d.pos[q].rcap = 0;
+        d.pos[q].ucap = u;
+        d.pos[q].cost = -x.cost * d.mult;
         d.ent[q] = 2 * s + 1;
         d.fwd[s] = p;
         if (low) {                      // lower-bound transform

@@ -50,7 +50,8 @@ class KsOpts(C.Structure):
                 ("walk_slack", C.c_int32), ("final_div", C.c_int32), ("pr_rounds", C.c_int32),
                 ("phase_exit", C.c_int32), ("phase_frac", C.c_int32), ("tail_sweeps", C.c_int32),
                 ("bf_margin", C.c_int32), ("two_hop", C.c_int32), ("log_cycles", C.c_int32),
-                ("fault_inject", C.c_int32), ("reserved", C.c_int32 * 8)]
+                ("fault_inject", C.c_int32), ("walk_passes", C.c_int32), ("tail_nodes", C.c_int32),
+                ("reserved", C.c_int32 * 6)]
 
 
 class KsResult(C.Structure):

@@ -143,7 +143,7 @@ def test_coalesced_stream_solves_like_the_raw_stream():
 def test_config4_full_size_rounds():
     """Config 4 at its stated size: the config-3 cell (100k tasks,
     10k machines, seed 3) under 5 % completions + 5 % arrivals per round, pins,
-    ageing and capacity refresh, three rounds through ks_apply_deltas. Every
+    ageing and capacity refresh, five rounds through ks_apply_deltas. Every
     round: bit-exact cost vs the cost-scaling oracle on the cell's full graph,
     the oracle's verifier accepts the downloaded flow, and every running task
     stays on its PU (graph_manager.go:675-720 pinning, :803-813 removal)."""
@@ -153,7 +153,7 @@ def test_config4_full_size_rounds():
         ctx.load_graph(cell.graph())
         ctx.solve()
         mp = ctx.task_mapping()
-        for rnd in range(3):
+        for rnd in range(5):
             d = cell.step(mp, done=T // 20, arrive=T // 20)
             ctx.apply_deltas(d)
             r = ctx.solve()
@@ -217,7 +217,9 @@ def test_deltas_applied_in_place_on_device():
             assert cst == 0 and (r.cost, r.flow) == (cost, flow), f"round {rnd + 1}"
             mp = ctx.task_mapping()
         assert rebuilt[0] == 1                 # the first stream switches the CSR to slack
-        assert sum(rebuilt[1:]) <= 3, rebuilt  # then the slack absorbs most rounds
+        # then inserts take the next free position or one a removed arc left inert
+        # (ks_store.hip claim_pos): the slack absorbs the churn round after round
+        assert sum(rebuilt[1:]) <= 1, rebuilt
 
 
 def test_batch_c_abi_gather_world1():
