@@ -115,10 +115,11 @@ typedef struct ks_opts {
                                   coarse slack at ε = 1 (may end non-1-optimal); bit 1 —
                                   the final prices are perturbed before verification.
                                   Both must be repaired by the certificate recovery.    */
-    int32_t  walk_passes;      /* blocking-flow walker passes per tail cycle [1]         */
-    int32_t  tail_nodes;       /* a phase's tail — blocking flows over each update, few
-                                  sweeps — starts once ≤ tail_nodes nodes hold excess
-                                  [64]; at most 4096                                    */
+    int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
+                                  cycle [1]; later passes retry units left short        */
+    int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —
+                                  starts once ≤ tail_nodes nodes hold excess [64]; at
+                                  most 4096                                             */
     int32_t  reserved[6];
 } ks_opts;
 

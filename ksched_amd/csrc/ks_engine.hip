@@ -40,11 +40,10 @@
 //              inbox; hub chunks claim excess with a CAS and the last-arriving
 //              chunk finalises the relabel. Bellman-Ford relaxations into a hub
 //              are min-reduced in LDS per workgroup.
-//   tail       once an update leaves ≤ 64 nodes with excess, a blocking flow
-//              over the update's distances (k_dfs_walk: one DFS walker per
-//              source with shared dead-end marks, hub excess split over many
-//              walkers via k_hub_cands) routes most of the remaining units in
-//              one kernel instead of one hop per sweep over dozens of cycles.
+//   tail       once an update leaves ≤ 64 nodes with excess, each sends its
+//              units down the update's distances (k_augment walks; k_aug_hub
+//              hands a hub's excess on in parallel) instead of one hop per
+//              sweep over dozens of cycles.
 //   verify     on-device: conservation, capacity, and 1-optimality of the final
 //              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
 //              the total cost is reduced in int64.
@@ -119,6 +118,7 @@ struct Ctl {
     int bf_seq0;           // sequence number of the running update's first (dense) round
     int aug_reached;       // walks of this cycle that reached a deficit / stopped short
     int aug_short;
+    int n_xl2;             // nodes fed by this cycle's hub distribution
     int dbg_x[4];          // diagnostics (KS_CYCLE_LOG): the first listed excess nodes, their excess at the apply
     int dbg_e[4];
 };
@@ -175,10 +175,8 @@ struct DG {
     const int* hnchunks;
     int* xl;               // excess nodes listed by the last apply (the first aug_k)
     int aug_k;             // a phase's tail: ≤ aug_k excess nodes (ks_opts.tail_nodes)
-    int* dead;             // per node: the walk stamp of the cycle that found it a dead end
-    int* hub_cand;         // per hub: qualifying out-arc positions (k_hub_cands), HC_CAP each
-    int* hub_cnt;          // per hub: entries listed this cycle
-    long long* hub_e;      // per hub: its excess when listed (the walkers' split)
+    int* xl2;              // nodes fed by k_aug_hub (the first AUG_K2)
+    long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
     long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
     long long* q_taken;
     long long* q_min;
@@ -1872,11 +1870,11 @@ __global__ void k_gu_max(DG g) {
     if (blockIdx.x == 0) {
         for (int k = threadIdx.x; k < MAXB; k += BLK) g.ctl->sweep_act[k] = 0;
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) {
-            g.hub_cnt[h] = 0;
-            g.hub_e[h] = 0;
+            g.aug_req[h] = 0;
         }
         if (threadIdx.x == 0) {
             g.ctl->apply_act = 0;
+            g.ctl->n_xl2 = 0;
         }
     }
     if (!g.ctl->bf_done) return;
@@ -1937,43 +1935,37 @@ __global__ void k_gu_apply(DG g, int sseq) {
 }
 
 // ------------------------------------------------------- tail augmentation ---
-// A phase's tail (≤ aug_k nodes hold excess after an update): a BLOCKING FLOW over
-// the update's distances instead of one hop per sweep. Measured on the CPU
-// (tools/proto/tail_proto.c, config 3's final phase): the last ~64 units have
-// augmenting paths of (near) zero length in ε units, but long, capacity-1 and
-// competing — matching-like chains — so a blocking flow (Hopcroft–Karp style: DFS
-// with dead-end marks) routes 37 of 64 units after the first update and all of
-// them after 7, where one augmenting path per update (successive shortest
-// paths, or greedy walks without backtracking) needed ~60.
+// When a converged update leaves at most aug_k nodes with excess (the tail of a
+// phase: a few units that the sweeps would move one hop per sweep over dozens
+// of update cycles), each of them sends its excess straight down the update's
+// distances: one wave per excess node walks from u along the residual arc
+// (u, w) of least distance d(w), until it reaches a deficit. An arc qualifies
+// if d(w) < d(u) (or d(w) = d(u) and it is admissible) and its reduced cost
+// under the updated prices is at most slack·ε: the reverse arc a push creates
+// then has reduced cost ≥ −slack·ε (slack 1 in a phase that must end
+// 1-optimal). Walkers claim residual capacity with a CAS (they may share arcs);
+// units that cannot go on (no arc, capacity taken, the hop limit) stay where the
+// walk stands, marked for the sweeps that follow; a unit that reaches a hub is
+// left there for the hub distribution (k_aug_hub), which hands it on along the
+// hub's qualifying arcs in parallel, and a second walker pass starts from the
+// nodes it fed. Runs between the apply and the cycle's sweeps.
 //
-// One wave per walker. A walker runs a DFS from its source along QUALIFYING arcs:
-// residual, head not marked dead this cycle, and either admissible (rc < 0) with
-// d(w) ≤ d(u), or rc ≤ slack·ε with d(w) < d(u) (d = the update's distances; the
-// arc of least d(w) first). Advancing claims one unit of the arc's residual with a
-// CAS; a node with no qualifying arc is marked dead (cycle-stamped, shared by all
-// walkers) and the walker retreats, giving the unit back. Reaching a deficit — or
-// a hub that has no candidate list — commits the path: the reverse residuals are
-// raised, the source gives its unit, the end node takes it. Reverse residuals are
-// raised only at commit, so no walker can use a tentative path's reverse arcs.
-// ε-optimality: a unit moves along arcs of rc ≤ slack·ε, so their reverses get rc
-// ≥ −slack·ε (slack 1 in a phase that must end 1-optimal).
-// Hubs (cluster aggregator): k_hub_cands lists a hub's qualifying out-arcs once
-// per cycle (its 100k-arc segment scanned by ~100 workgroups), and walkers scan
-// that list instead; the hub's excess is split over HUB_W walkers, one unit
-// stream each.
-constexpr int DFS_PATH = 512;     // path stack (positions) per walker
-constexpr int DFS_STEPS = 4096;   // advance / retreat steps per walker and cycle
-constexpr int HC_CAP = 4096;      // candidate out-arcs listed per hub
-constexpr int HUB_W = 192;        // walkers sharing a hub's excess
+// Measured alternative, not kept: a blocking flow (DFS walkers with
+// dead-end marks). On the device's own tail state (a -DKS_DUMP snapshot read by
+// tools/proto/tail_dump.c) even a sequential blocking flow needs 21–24 updates
+// for config 3's last 68 units — the last ones leave two nodes one unit per
+// update through the cluster aggregator — so it saved no cycles and its searches
+// cost more than these walks.
+constexpr int AUG_K2 = 256;        // walkers from the nodes a hub distribution fed
+constexpr int AUG_STEPS = 512;     // hops per walk before its units are left where it stands
 
-__device__ __forceinline__ bool walk_ok(long long rc, long long dw, long long du, long long L, long long eps,
-                                        int slack) {
-    const bool down = dw < du || du >= L;
-    return (rc < 0 && (dw <= du || du >= L)) || (rc <= slack * eps && down);
-}
-
-// Per hub chunk: a hub holding excess lists its qualifying out-arcs (non-hub heads).
-__global__ __launch_bounds__(BLK) void k_hub_cands(DG g, int slack) {
+// Hub distribution (between the two walker passes): a hub that holds excess
+// hands it to its qualifying arcs, one workgroup per chunk claiming its share
+// with one returning atomic (as the sweeps' hub chunks do); the fed nodes are
+// listed for the second walker pass.
+__global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
+    __shared__ long long sh[WPB];
+    __shared__ long long s_take;
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
     if (nx == 0 || nx > g.aug_k) return;
@@ -1981,182 +1973,172 @@ __global__ __launch_bounds__(BLK) void k_hub_cands(DG g, int slack) {
     const int x = it.node;
     const long long E = atom_load(&g.excess[x]);
     if (E <= 0) return;
-    if (it.begin == g.first[x] && threadIdx.x == 0) g.hub_e[it.hid] = E;   // snapshot for the split
-    const long long eps = g.ctl->eps, L = g.ctl->gu_L;
+    const Front F = g.sf[sseq % 3];
+    const long long eps = g.ctl->eps;
     const long long dx = atom_load(&g.dist[ni(x)]);
     const long long px = g.p0[ni(x)];
+    long long r[PER_T], adm[PER_T], uc[PER_T];
+    int w[PER_T], rv[PER_T];
+    long long mine = 0;
+#pragma unroll
     for (int k = 0; k < PER_T; ++k) {
-        const int a = it.begin + k * BLK + (int)threadIdx.x;
-        bool q = false;
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        r[k] = 0;
+        w[k] = 0;
+        rv[k] = 0;
+        uc[k] = 0;
+        adm[k] = 0;
         if (a < it.end) {
-            const Pos r = ld_pos(g.pos + a);
-            if (r.rcap > 0 && r.head < g.hub_base) {
-                const long long rc = r.cost + px - g.p0[ni(r.head)];
-                q = walk_ok(rc, atom_load(&g.dist[ni(r.head)]), dx, L, eps, slack);
+            const Pos q = ld_pos(g.pos + a);
+            r[k] = atom_load(&g.pos[a].rcap);   // the first walker pass claimed with atomics
+            w[k] = q.head;
+            rv[k] = q.rev;
+            uc[k] = q.ucap;
+            if (r[k] > 0) {
+                const long long cr = q.cost + px - g.p0[ni(q.head)];
+                const long long dw = atom_load(&g.dist[ni(q.head)]);
+                if (cr <= slack * eps && (dw < dx || (dw == dx && cr < 0))) adm[k] = r[k];
             }
         }
-        const unsigned long long m = __ballot(q);
-        if (!m) continue;
-        int base = 0;
-        if (lane_id() == 0) base = atomicAdd(&g.hub_cnt[it.hid], (int)__popcll(m));
-        base = __shfl(base, 0);
-        const int idx = base + (int)__popcll(m & ((1ULL << lane_id()) - 1));
-        if (q && idx < HC_CAP) g.hub_cand[it.hid * HC_CAP + idx] = a;
+        mine += adm[k];
+    }
+    long long Ac = 0;
+    const long long excl = block_excl_scan(mine, sh, &Ac);
+    if (threadIdx.x == 0) {
+        long long take = 0;
+        if (Ac > 0) {
+            const long long start = atom_add_ret(&g.aug_req[it.hid], Ac);
+            take = E - start;
+            take = take < 0 ? 0 : (take > Ac ? Ac : take);
+        }
+        s_take = take;
+        if (take) atom_add(&g.excess[x], -take);
+    }
+    __syncthreads();
+    long long rt = s_take - excl;
+    rt = rt < 0 ? 0 : (rt > mine ? mine : rt);
+    int dummy = 0;
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+        const long long d = adm[k] < rt ? adm[k] : rt;
+        rt -= d;
+        if (d <= 0) continue;
+        const int a = it.begin + threadIdx.x * PER_T + k;
+        g.pos[a].rcap = r[k] - d;              // only this chunk touches the pair in this kernel
+        g.pos[rv[k]].rcap = uc[k] - (r[k] - d);
+        const long long now = atom_add_ret(&g.excess[w[k]], d) + d;
+        if (now > 0) {
+            mark(g, F, w[k], dummy);
+            const int idx = atomicAdd(&g.ctl->n_xl2, 1);
+            if (idx < AUG_K2) g.xl2[idx] = w[k];
+        }
     }
 }
 
-// The DFS walkers: blocks [0, aug_k) start at the listed non-hub excess nodes (all
-// their units, one path each), blocks [aug_k, aug_k + HUB_W) share the excess of the
-// first hub that had some (k_hub_cands' snapshot).
-__global__ __launch_bounds__(WAVE) void k_dfs_walk(DG g, int sseq, int slack, int stamp) {
+// mode 0: from the apply's excess nodes (non-hubs); mode 1: from the nodes a hub
+// distribution (k_aug_hub) fed.
+__global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int slack) {
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
     if (nx == 0 || nx > g.aug_k) return;
-    __shared__ int path[DFS_PATH];
+    const int cnt = mode ? min(g.ctl->n_xl2, AUG_K2) : nx;
+    if ((int)blockIdx.x >= cnt) return;
     const int lane = lane_id();
     const Front F = g.sf[sseq % 3];
-    const long long eps = g.ctl->eps, L = g.ctl->gu_L;
-    int s = -1, hs = -1;          // source node; its hub index when it is a hub
-    long long units = 0;
-    if ((int)blockIdx.x < g.aug_k) {
-        if ((int)blockIdx.x >= nx) return;
-        s = g.xl[blockIdx.x];
-        if (s < 0 || s >= g.hub_base) return;
-        units = atom_load(&g.excess[s]);
-    } else {
-        const int k = (int)blockIdx.x - g.aug_k;
-        for (int h = 0; h < g.nheavy && h < HUB_LDS; ++h) {
-            const long long E = atom_load(&g.hub_e[h]);
-            if (E <= 0 || atom_load_i(&g.hub_cnt[h]) <= 0) continue;
-            const long long nw = E < HUB_W ? E : HUB_W;
-            if (k < nw) {
-                s = g.hub_base + h;
-                hs = h;
-                units = E / nw + (k < E % nw ? 1 : 0);
-            }
-            break;
-        }
-        if (s < 0) return;
+    const long long eps = g.ctl->eps;
+    int u = mode ? g.xl2[blockIdx.x] : g.xl[blockIdx.x];
+    if (u < 0 || u >= g.hub_base) return;   // hubs: k_aug_hub
+    long long carry = 0;
+    if (lane == 0) carry = atom_exch(&g.excess[u], 0LL);
+    carry = __shfl(carry, 0);
+    if (carry <= 0) {
+        if (lane == 0 && carry < 0) atom_add(&g.excess[u], carry);   // (not an excess node any more)
+        return;
     }
-    int dummy = 0, reached = 0, steps = 0, hops = 0;
-    long long left = units;
-    while (left > 0 && steps < DFS_STEPS) {
-        // one DFS from s for one unit
-        int plen = 0, u = s, t = -1;
-        bool fail = false;
-        while (steps < DFS_STEPS) {
-            ++steps;
-            const bool uhub = u >= g.hub_base;
-            const int uh = u - g.hub_base;
-            if (u != s) {
-                const long long eu = atom_load(&g.excess[u]);
-                const bool no_list =
-                    uhub && (uh >= HUB_LDS || atom_load(&g.hub_e[uh]) <= 0 || atom_load_i(&g.hub_cnt[uh]) <= 0);
-                if (eu < 0 || no_list) {   // a deficit, or a hub without a candidate list: deposit there
-                    t = u;
+    long long du = atom_load(&g.dist[ni(u)]);
+    long long pu = g.p0[ni(u)];
+    int hops = 0, reached = 0, dummy = 0;
+    for (int step = 0; step < AUG_STEPS; ++step) {
+        int b0, en;
+        seg_of(g.p0, u, b0, en);
+        // the qualifying residual arc of least d(w) (ties: lowest position)
+        long long bd = INF64;
+        int ba = -1;
+        for (int base = b0; base < en; base += WAVE) {
+            const int a = base + lane;
+            long long key = INF64;
+            if (a < en) {
+                const Pos q = ld_pos(g.pos + a);
+                const long long r = atom_load(&g.pos[a].rcap);   // other walkers claim with atomics
+                const long long cr = q.cost + pu - g.p0[ni(q.head)];
+                const long long dw = atom_load(&g.dist[ni(q.head)]);
+                if (r > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
+            }
+            const long long mn = wave_min(key);
+            if (mn < bd) {
+                const unsigned long long hit = __ballot(key == mn);
+                bd = mn;
+                ba = base + __ffsll((long long)hit) - 1;
+            }
+        }
+        if (ba < 0) break;
+        // claim min(carry, residual) on arc ba
+        long long take = 0;
+        int w = 0;
+        if (lane == 0) {
+            w = g.pos[ba].head;
+            long long r = atom_load(&g.pos[ba].rcap);
+            for (;;) {
+                take = r < carry ? r : carry;
+                if (take <= 0) {
+                    take = 0;
                     break;
                 }
+                long long exp = r;
+                if (__hip_atomic_compare_exchange_strong(&g.pos[ba].rcap, &exp, r - take, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    break;
+                r = exp;
             }
-            const long long du = atom_load(&g.dist[ni(u)]);
-            const long long pu = g.p0[ni(u)];
-            // the qualifying arc of least d(w) (ties: lowest index)
-            long long bd = INF64;
-            int ba = -1;
-            int lo, hi;
-            const int* cand = nullptr;
-            if (uhub) {
-                cand = g.hub_cand + uh * HC_CAP;
-                lo = 0;
-                hi = min(atom_load_i(&g.hub_cnt[uh]), HC_CAP);
-            } else {
-                seg_of(g.p0, u, lo, hi);
+            if (take > 0) atom_add(&g.pos[g.pos[ba].rev].rcap, take);
+            if (take < carry) {   // the rest stays at u
+                atom_add(&g.excess[u], carry - take);
+                mark(g, F, u, dummy);
             }
-            // hub walkers spread over the list: each starts its scan at its own chunk
-            const int n_it = (hi - lo + WAVE - 1) / WAVE;
-            const int rot = uhub ? (int)blockIdx.x % max(1, n_it) : 0;
-            for (int it = 0; it < n_it; ++it) {
-                const int i = lo + ((it + rot) % n_it) * WAVE + lane;
-                long long key = INF64;
-                int a = -1;
-                if (i < hi) {
-                    a = cand ? cand[i] : i;
-                    const Pos r = ld_pos(g.pos + a);
-                    const long long rr = atom_load(&g.pos[a].rcap);   // claims by other walkers
-                    const int w = r.head;
-                    if (rr > 0 && w != u && g.dead[w] != stamp) {
-                        const long long dw = atom_load(&g.dist[ni(w)]);
-                        if (walk_ok(r.cost + pu - g.p0[ni(w)], dw, du, L, eps, slack)) key = dw;
-                    }
-                }
-                const long long mn = wave_min(key);
-                if (mn < bd) {
-                    const unsigned long long hit = __ballot(key == mn);
-                    bd = mn;
-                    ba = __shfl(a, __ffsll((long long)hit) - 1);
-                }
-                if (uhub && bd < INF64) break;   // at a hub the first chunk with a candidate will do
-            }
-            bool adv = false;
-            if (ba >= 0 && plen < DFS_PATH) {
-                int ok = 0;
-                if (lane == 0) {   // claim one unit of the arc
-                    long long r = atom_load(&g.pos[ba].rcap);
-                    while (r > 0) {
-                        long long exp = r;
-                        if (__hip_atomic_compare_exchange_strong(&g.pos[ba].rcap, &exp, r - 1, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                            ok = 1;
-                            break;
-                        }
-                        r = exp;
-                    }
-                }
-                adv = __shfl(ok, 0) != 0;
-                if (!adv) continue;   // lost the race for it: scan u again
-            }
-            if (adv) {
-                if (lane == 0) path[plen] = ba;
-                __syncthreads();
-                ++plen;
-                u = g.pos[ba].head;
-                continue;
-            }
-            // no qualifying arc: u is a dead end this cycle
-            if (lane == 0) g.dead[u] = stamp;
-            if (plen == 0) {
-                fail = true;   // the source itself: its units stay
-                break;
-            }
-            const int a = path[--plen];
-            if (lane == 0) atom_add(&g.pos[a].rcap, 1LL);   // give the unit back
-            u = g.pos[g.pos[a].rev].head;
         }
-        if (t < 0) {   // no path (or out of steps): release what the DFS still holds
-            for (int i = lane; i < plen; i += WAVE) atom_add(&g.pos[path[i]].rcap, 1LL);
-            fail = true;
-        } else {       // commit: reverse residuals, the unit from s to t
-            for (int i = lane; i < plen; i += WAVE) atom_add(&g.pos[g.pos[path[i]].rev].rcap, 1LL);
-            if (lane == 0) {
-                atom_add(&g.excess[s], -1LL);
-                const long long now = atom_add_ret(&g.excess[t], 1LL) + 1;
-                if (now > 0) mark(g, F, t, dummy);   // overfilled deficit / hub deposit: the sweeps take it
-            }
-            hops += plen;
-            reached += t >= 0 && atom_load(&g.excess[t]) <= 0;
-            --left;
+        take = __shfl(take, 0);
+        w = __shfl(w, 0);
+        if (take == 0) {
+            carry = 0;   // deposited at u above
+            break;
         }
-        __syncthreads();
-        if (fail) break;
+        carry = take;
+        ++hops;
+        u = w;
+        du = bd;
+        if (lane == 0) {
+            const long long e = atom_load(&g.excess[u]);
+            if (e < 0 || u >= g.hub_base) {   // a deficit (or a hub: the hub distribution takes over)
+                const long long now = atom_add_ret(&g.excess[u], carry) + carry;
+                if (now > 0) mark(g, F, u, dummy);
+                reached = e < 0 ? 1 : 0;
+                carry = 0;
+            }
+        }
+        carry = __shfl(carry, 0);
+        if (carry == 0) break;
+        pu = g.p0[ni(u)];
     }
     if (lane == 0) {
-        if (left > 0) mark(g, F, s, dummy);   // the units that found no path stay (sweeps)
+        if (carry > 0) {   // hop limit or no qualifying arc: the units stay at u
+            atom_add(&g.excess[u], carry);
+            mark(g, F, u, dummy);
+        }
         const int sh = (int)blockIdx.x & (CTR_SHARDS - 1);
-        atomicAdd(units - left > 0 ? &g.ctl->aug_reached : &g.ctl->aug_short, 1);
-        if (units - left > 0) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, (unsigned long long)(units - left));
+        atomicAdd(reached ? &g.ctl->aug_reached : &g.ctl->aug_short, 1);
+        if (reached) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, 1ULL);
         if (hops) atomicAdd(g.ctr + sh * NCTR + C_AUGHOP, (unsigned long long)hops);
     }
-    (void)hs;
-    (void)reached;
 }
 
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
@@ -2577,10 +2559,8 @@ struct EngineImpl {
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
-    DBuf<int> xl;                      // walker start nodes (k_dfs_walk)
-    DBuf<int> dead, hub_cand, hub_cnt; // walkers: dead-end stamps, hub candidate lists
-    DBuf<long long> hub_e;
-    int walk_stamp = 0;                // per cycle (dead-end marks)
+    DBuf<int> xl, xl2;                 // walker start nodes (k_augment)
+    DBuf<long long> aug_req;           // per hub claim counter (k_aug_hub)
     DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;        // pinned host mirror
@@ -2647,7 +2627,7 @@ struct EngineImpl {
         for (auto& b : cls_list) b.release();
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
         q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
-        flags.release(); hubflags.release(); ctr.release(); xl.release(); dead.release(); hub_cand.release(); hub_cnt.release(); hub_e.release(); ctl.release(); saved_flows.release(); p_slot.release();
+        flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
@@ -2733,10 +2713,8 @@ struct EngineImpl {
         g.nheavy = nheavy;
         g.hnchunks = hnchunks.p;
         g.xl = xl.p;
-        g.dead = dead.p;
-        g.hub_cand = hub_cand.p;
-        g.hub_cnt = hub_cnt.p;
-        g.hub_e = hub_e.p;
+        g.xl2 = xl2.p;
+        g.aug_req = aug_req.p;
         g.q_req = q_req.p;
         g.q_taken = q_taken.p;
         g.q_min = q_min.p;
@@ -2807,6 +2785,7 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     KS_CHECK(s.ctl.ensure(1));
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
     KS_CHECK(s.xl.ensure(AUG_KMAX));
+    KS_CHECK(s.xl2.ensure(AUG_K2));
     KS_CHECK(s.sctl.ensure(1));
     KS_CHECK(hipMemset(s.sctl.p, 0, sizeof(StoreCtl)));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
@@ -3172,14 +3151,8 @@ static int build(EngineImpl& s, std::string& err) {
             KS_CHECK(hipMemcpyAsync(s.citems.p, ci.data(), ci.size() * sizeof(CItem), hipMemcpyHostToDevice, st));
         const int nq = std::max(1, s.nheavy);
         KS_CHECK(s.q_req.ensure(nq));
-        KS_CHECK(s.hub_cand.ensure((size_t)nq * HC_CAP));
-        KS_CHECK(s.hub_cnt.ensure(nq));
-        KS_CHECK(s.hub_e.ensure(nq));
-        KS_CHECK(hipMemsetAsync(s.hub_cnt.p, 0, nq * sizeof(int), st));
-        KS_CHECK(hipMemsetAsync(s.hub_e.p, 0, nq * sizeof(long long), st));
-        KS_CHECK(s.dead.ensure(std::max(1, s.nn)));
-        KS_CHECK(hipMemsetAsync(s.dead.p, 0, std::max(1, s.nn) * sizeof(int), st));
-        s.walk_stamp = 0;
+        KS_CHECK(s.aug_req.ensure(nq));
+        KS_CHECK(hipMemsetAsync(s.aug_req.p, 0, nq * sizeof(long long), st));
         KS_CHECK(s.q_taken.ensure(nq));
         KS_CHECK(s.q_min.ensure(nq));
         KS_CHECK(s.q_unsat.ensure(nq));
@@ -3803,16 +3776,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
-            if (use_aug) {   // tail: a blocking flow over the update's distances (DFS walkers)
-                if (nhit) hipLaunchKernelGGL(k_hub_cands, dim3(nhit), dim3(BLK), 0, st, g, walk_sl);
-                for (int wp = 0; wp < walk_passes; ++wp) {
-                    if (++s.walk_stamp >= (1 << 30)) {   // (never in practice) restart the stamps
-                        s.walk_stamp = 1;
-                        (void)hipMemsetAsync(s.dead.p, 0, std::max(1, nn) * sizeof(int), st);
-                    }
-                    hipLaunchKernelGGL(k_dfs_walk, dim3(g.aug_k + HUB_W), dim3(WAVE), 0, st, g, sseq, walk_sl,
-                                       s.walk_stamp);
-                }
+            if (use_aug) {   // tail: walkers, hub distribution, walkers from what it fed
+                hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
+                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, walk_sl);
+                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, walk_sl);
+                // further passes retry the units left short at the listed nodes
+                for (int wp = 1; wp < walk_passes; ++wp)
+                    hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
@@ -3859,6 +3829,39 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
                 std::fprintf(stderr, "\n");
             }
+#ifdef KS_DUMP
+            // diagnostic builds: the residual state at the first tail cycle of a final
+            // phase (tools/proto/tail_dump.c reads it)
+            if (!may_end_early && hc->n_exc > 0 && hc->n_exc <= g.aug_k) {
+                static int dumped = 0;
+                const char* path = std::getenv("KS_DUMP");
+                if (path && !dumped++) {
+                    (void)hipStreamSynchronize(st);
+                    const long long nposn = s.m2cap, nnode = nn, nh = s.nheavy;
+                    std::vector<Pos> hp(nposn);
+                    std::vector<long long> hnd(4 * (size_t)nnode), hex(nnode), hib((size_t)nh * SHARDS);
+                    std::vector<int> hf(nnode + 1);
+                    (void)hipMemcpy(hp.data(), s.pos.p, nposn * sizeof(Pos), hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(hnd.data(), s.nd.p, hnd.size() * 8, hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(hex.data(), s.excess.p, hex.size() * 8, hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(hf.data(), s.first.p, hf.size() * 4, hipMemcpyDeviceToHost);
+                    if (nh) (void)hipMemcpy(hib.data(), s.inbox.p, hib.size() * 8, hipMemcpyDeviceToHost);
+                    for (long long h = 0; h < nh; ++h)
+                        for (int k = 0; k < SHARDS; ++k) hex[s.hub_base + h] += hib[h * SHARDS + k];
+                    if (FILE* f = std::fopen(path, "wb")) {
+                        const long long hdr[6] = {nnode, (long long)s.hub_base, nposn, eps_ph, mult, (long long)hc->n_exc};
+                        std::fwrite(hdr, 8, 6, f);
+                        std::fwrite(hf.data(), 4, hf.size(), f);
+                        std::fwrite(hnd.data(), 8, hnd.size(), f);
+                        std::fwrite(hex.data(), 8, hex.size(), f);
+                        std::fwrite(hp.data(), sizeof(Pos), hp.size(), f);
+                        std::fclose(f);
+                        std::fprintf(stderr, "KS_DUMP: wrote %s (n %lld, positions %lld, eps %lld)\n", path, nnode,
+                                     nposn, eps_ph);
+                    }
+                }
+            }
+#endif
             kb = std::max(kb_min, std::min(256, hc->bf_count - hc->bf_r0 + kb_margin));
             ++gus;
             sweeps += gi;

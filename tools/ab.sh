@@ -9,8 +9,10 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 for r in $(seq 1 "$ROUNDS"); do
     for v in "$@"; do
-        name=$(echo "$v" | tr ',=' '_-')
-        if [[ "$v" == *=* ]]; then
+        name=$(echo "$v" | sed 's/[,=@:+]/_/g')
+        if [[ "$v" == *@* ]]; then   # lib@K=V[,K=V]: a library variant with environment settings
+            lib="KS_LIB_VARIANT=${v%%@*}"; envs=$(echo "${v#*@}" | tr ',' ' ')
+        elif [[ "$v" == *=* ]]; then
             envs=$(echo "$v" | tr ',' ' '); lib=""
         elif [ "$v" = default ]; then envs=""; lib=""
         else envs=""; lib="KS_LIB_VARIANT=$v"

@@ -97,6 +97,8 @@ int main(int argc, char** argv) {
              * admissible arcs toward no larger distance (rc' < 0, d(w) <= d(u), residual) */
             int64_t gus = 0, moved_total = 0;
             char* dead = calloc(n, 1);
+            const int hub_rule = getenv("HUB_RULE") != NULL;
+            const int unit = getenv("UNIT") != NULL;
             int64_t* stk = malloc(8 * (n + 1));
             for (;;) {
                 int64_t nx = 0;
@@ -134,6 +136,11 @@ int main(int argc, char** argv) {
                         int64_t* path = malloc(8 * 4096); int64_t plen = 0;
                         for (int steps = 0; steps < 100000; ++steps) {
                             if (r.ex[u] < 0 && u != s0) { found = u; break; }
+                            if (hub_rule && u != s0 && r.first[u + 1] - r.first[u] > 4096 && r.ex[u] <= 0) {
+                                dead[u] = 1;   /* HUB_RULE: a hub without excess is a dead end (device list rule) */
+                                u = r.head[r.rev[path[--plen]]];
+                                continue;
+                            }
                             int64_t best = -1, bd = INF;
                             for (int64_t a = r.first[u]; a < r.first[u + 1]; ++a) {
                                 if (r.rcap[a] <= 0) continue;
@@ -156,6 +163,7 @@ int main(int argc, char** argv) {
                         }
                         if (found < 0) { free(path); break; }
                         int64_t delta = r.ex[s0] < -r.ex[found] ? r.ex[s0] : -r.ex[found];
+                        if (unit) delta = 1;
                         for (int64_t i = 0; i < plen; ++i) if (r.rcap[path[i]] < delta) delta = r.rcap[path[i]];
                         for (int64_t i = 0; i < plen; ++i) { r.rcap[path[i]] -= delta; r.rcap[r.rev[path[i]]] += delta; }
                         r.ex[s0] -= delta; r.ex[found] += delta; moved += delta;
