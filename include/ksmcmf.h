@@ -120,7 +120,14 @@ typedef struct ks_opts {
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —
                                   starts once ≤ tail_nodes nodes hold excess [64]; at
                                   most 4096                                             */
-    int32_t  reserved[6];
+    int32_t  bf_bound;         /* a global update with ≤ 64 excess nodes drops Bellman-Ford
+                                  offers at or above the largest tentative distance of
+                                  those nodes and caps prices there [on]; < 0 off       */
+    int32_t  fwd_nodes;        /* once ≤ fwd_nodes nodes hold excess, a cycle searches
+                                  from them to the nearest deficit and pushes along the
+                                  search's shortest paths instead of a global update
+                                  [0 = off]                                             */
+    int32_t  reserved[4];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */

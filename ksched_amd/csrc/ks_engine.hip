@@ -101,6 +101,14 @@ constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-conv
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7 };
 constexpr int AUG_KMAX = 4096;     // most excess nodes a tail's walkers start from (ks_opts.tail_nodes)
+constexpr int BX_CAP = 64;         // global updates with at most this many excess nodes are bounded
+// Forward tail update: a node's search key (in its record's dist slot) packs the
+// distance from the excess nodes above the position of the arc that set it.
+constexpr int FS_PB = 26;
+constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess node)
+constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
+constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
+constexpr int FS_LIST_BLOCKS = 128;
 
 struct Ctl {
     long long eps;
@@ -121,6 +129,18 @@ struct Ctl {
     int n_xl2;             // nodes fed by this cycle's hub distribution
     int dbg_x[4];          // diagnostics (KS_CYCLE_LOG): the first listed excess nodes, their excess at the apply
     int dbg_e[4];
+    int n_bx;              // excess nodes k_gu_init listed for the distance bound (> BX_CAP: no bound)
+    long long bf_bound;    // Bellman-Ford prune bound: max tentative distance of the listed excess nodes
+    long long gu_B;        // the converged bounded update's cap: max distance of the listed excess nodes
+    // forward tail update (k_fs_*): a search from the excess nodes
+    long long fs_D;        // least distance of a deficit found by the running search (INF64: none yet)
+    int fs_cnt[3];         // frontier list lengths (rotating like the flag buffers)
+    int fs_done;           // the search's frontier drained
+    int fs_fail;           // list overflow or no deficit in range: the next cycle is a backward update
+    int fs_pending;        // the search has not converged: the next cycle continues it
+    int fs_rounds;         // rounds of the running search that had a frontier
+    int n_fdef;            // deficits at distance D listed for the trace
+    int fs_moved;          // units the trace moved
 };
 
 struct HItem {
@@ -176,6 +196,11 @@ struct DG {
     int* xl;               // excess nodes listed by the last apply (the first aug_k)
     int aug_k;             // a phase's tail: ≤ aug_k excess nodes (ks_opts.tail_nodes)
     int* xl2;              // nodes fed by k_aug_hub (the first AUG_K2)
+    int* bx;               // excess nodes of the running update (the first BX_CAP; k_gu_init)
+    int* fl;               // forward search: 3 rotating frontier lists of fl_cap node ids
+    int fl_cap;
+    int* fdef;             // forward search: deficits at the found distance (FDEF_CAP)
+    int bound;             // 1: prune Bellman-Ford offers at ctl->bf_bound (ks_opts.bf_bound >= 0)
     long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
     long long* q_req;      // claim slots: hubs [0, nheavy), then chunked nodes
     long long* q_taken;
@@ -1409,7 +1434,8 @@ __device__ __forceinline__ long long arc_len(long long pu, long long ca, long lo
 // distance this call lowered (the caller then owns propagating it).
 template <bool PR>
 __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long long cand, long long du,
-                                      long long* hub_min, int& out) {
+                                      long long B, long long* hub_min, int& out) {
+    if (cand >= B) return false;   // at or beyond every listed excess node's distance (bounded update)
     if (u >= g.hub_base) {
         const int h = u - g.hub_base;
         if (h < HUB_LDS) {
@@ -1432,11 +1458,11 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 #endif
 template <bool PR>
 __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
-                           long long* hub_min, int& out);
+                           long long B, long long* hub_min, int& out);
 
 template <bool PR, bool MID = (KS_HOP3 != 0)>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
-                                            int b0, int b1, long long eps, long long* hub_min, int& out) {
+                                            int b0, int b1, long long eps, long long B, long long* hub_min, int& out) {
     // the records of all (≤ 8) arcs issued together; usually one in-arc carries
     // flow (a task's assignment), so the dependent loads follow for it alone
     unsigned live = 0;
@@ -1457,7 +1483,7 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         if (g.pos[b].ucap - g.pos[b].rcap > 0) {
             const int u2 = g.pos[b].head;
             const long long cand = du + arc_len<PR>(g.p0[ni(u2)], g.pos[b].cost, pu, eps);
-            if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, hub_min, out)) {
+            if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, B, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
             }
@@ -1476,9 +1502,9 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         const long long pu2 = g.p0[ni(u2)];
         const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
         const long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
-        if (offer<PR>(g, nf, u2, cand, du2, hub_min, out)) {
+        if (offer<PR>(g, nf, u2, cand, du2, B, hub_min, out)) {
             if (MID && u2 >= g.obeg[2] && u2 < g.obeg[4]) {
-                expand_mid<PR>(g, nf, u2, cand, pu2, eps, hub_min, out);   // a machine: two more hops
+                expand_mid<PR>(g, nf, u2, cand, pu2, eps, B, hub_min, out);   // a machine: two more hops
             } else {
                 nf.flag[u2] = 1;
                 out = 1;
@@ -1492,7 +1518,7 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
 // machine ← task ← machine ← task path advances two displacements per round.
 template <bool PR>
 __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
-                           long long* hub_min, int& out) {
+                           long long B, long long* hub_min, int& out) {
     int b0, b1;
     seg_of(g.p0, u, b0, b1);
     for (int base = b0; base < b1; base += 8) {
@@ -1524,11 +1550,11 @@ __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, lo
             const long long pu3 = g.p0[ni(u3)];
             const long long du3 = u3 < g.hub_base ? g.dist[ni(u3)] : INF64;
             const long long cand = du + arc_len<PR>(pu3, c3, pu, eps);
-            if (!offer<PR>(g, nf, u3, cand, du3, hub_min, out)) continue;
+            if (!offer<PR>(g, nf, u3, cand, du3, B, hub_min, out)) continue;
             if (g.expand && u3 < g.obeg[2]) {
                 int e0, e1;
                 seg_of(g.p0, u3, e0, e1);
-                expand_leaf<PR, false>(g, nf, u3, cand, pu3, e0, e1, eps, hub_min, out);
+                expand_leaf<PR, false>(g, nf, u3, cand, pu3, e0, e1, eps, B, hub_min, out);
             } else {
                 nf.flag[u3] = 1;
                 out = 1;
@@ -1541,7 +1567,7 @@ __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, lo
 // cost −cost(a). Loads are issued before the residual test (short chain).
 template <bool PR>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
-                                         long long eps, long long* hub_min, int& out) {
+                                         long long eps, long long B, long long* hub_min, int& out) {
     const Pos q = ld_pos(g.pos + a);
     const long long rin = q.ucap - q.rcap;
     const int u = q.head;
@@ -1553,9 +1579,9 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     if (leaf) seg_of(g.p0, u, b0, b1);   // same record line as pu, du
     if (rin <= 0) return;
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
-    if (!offer<PR>(g, nf, u, cand, du, hub_min, out)) return;
+    if (!offer<PR>(g, nf, u, cand, du, B, hub_min, out)) return;
     if (leaf) {
-        expand_leaf<PR>(g, nf, u, cand, pu, b0, b1, eps, hub_min, out);   // tasks, PUs: two hops per round
+        expand_leaf<PR>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
     } else {
         nf.flag[u] = 1;
         out = 1;
@@ -1564,7 +1590,7 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
 
 template <int G, bool PR>
 __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v, long long dv, long long pv, int b0,
-                                             int en, long long eps, long long* hub_min, int& out, long long& scans) {
+                                             int en, long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
     const bool act = v >= 0 && (PR || dv < INF64);
     if (!act) en = b0;
@@ -1572,7 +1598,7 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR>(g, nf, a, dv, pv, eps, hub_min, out);
+            relax_in<PR>(g, nf, a, dv, pv, eps, B, hub_min, out);
             scans++;
         }
     }
@@ -1581,7 +1607,7 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
 // Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
 template <int C, bool PR>
 __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, const WinFlag& f,
-                                       long long eps, long long* hub_min, int& out, long long& scans) {
+                                       long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     constexpr int G = class_lanes(C);
     constexpr int PER = 64 / G;
     constexpr int WS = win_slots(C);
@@ -1601,7 +1627,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
             seg_of(g.p0, v, b0, en);
         }
         if (v < 0) d = INF64;
-        bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, hub_min, out, scans);
+        bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
 }
@@ -1609,18 +1635,18 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
 // One 64-arc chunk of a chunked-class node (its flag already tested).
 template <bool PR>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
-                                         long long* hub_min, int& out, long long& scans) {
+                                         long long B, long long* hub_min, int& out, long long& scans) {
     const long long dv = atom_load(&g.dist[ni(ci.node)]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
-        relax_in<PR>(g, N, a, dv, g.p0[ni(ci.node)], eps, hub_min, out);
+        relax_in<PR>(g, N, a, dv, g.p0[ni(ci.node)], eps, B, hub_min, out);
         scans++;
     }
 }
 
 template <int G, bool PR>
-__device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long* hub_min,
+__device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long B, long long* hub_min,
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
     long long dv = INF64;
@@ -1636,7 +1662,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR>(g, nf, a, dv, pv, eps, hub_min, out);
+            relax_in<PR>(g, nf, a, dv, pv, eps, B, hub_min, out);
             scans++;
         }
     }
@@ -1669,6 +1695,9 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
     int kind = (int)blockIdx.x < g.nhitems * HSPLIT ? 1 : 0;
 #endif
     const long long eps = g.ctl->eps;
+    // bounded update (tail): offers at or above the listed excess nodes' largest
+    // tentative distance are dropped (that bound only falls, so a stale copy is safe)
+    const long long B = (!PR && g.bound) ? atom_load(&g.ctl->bf_bound) : INF64;
     int out = 0;
     long long scans = 0;
     // Hub chunks are split over HSPLIT workgroups: a relaxation is a dependent
@@ -1689,7 +1718,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR>(g, N, a, dv, pv, eps, hub_min, out);
+                        relax_in<PR>(g, N, a, dv, pv, eps, B, hub_min, out);
                         scans++;
                     }
                 }
@@ -1702,11 +1731,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             // the update already converged
         } else if (w < g.wbeg[CCLS]) {
             const Scan sc{F.flag, 1};
-#define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, hub_min, out, scans)
+#define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, B, hub_min, out, scans)
             KS_BY_CLASS(w, sc, KS_BF_CALL)
 #undef KS_BF_CALL
         } else if (w - g.wbeg[CCLS] < g.ncitems) {
-            bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
+            bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
         }
     } else {
         const int tw = ((int)gridDim.x - nhb) * WPB;
@@ -1738,7 +1767,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
-                bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, hub_min, out, scans);
+                bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
 #ifdef KS_STAMPS
                 kind = max(kind, 2);
 #endif
@@ -1748,11 +1777,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             kind = max(kind, 3 + class_of_window(g, w));
 #endif
             switch (class_of_window(g, w)) {
-                case 0: bf_win<0, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
-                case 1: bf_win<1, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
-                case 2: bf_win<2, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
-                case 3: bf_win<3, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
-                default: bf_win<4, PR>(g, N, w, mk[j], wf[j], eps, hub_min, out, scans); break;
+                case 0: bf_win<0, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 1: bf_win<1, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 2: bf_win<2, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 3: bf_win<3, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                default: bf_win<4, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
             }
         }
     }
@@ -1774,6 +1803,18 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             g.ctl->bf_count += 1;
         } else if (!done) {
             g.ctl->bf_done = 1;   // empty frontier: the update converged
+        }
+    }
+    // the next rounds' bound: the largest tentative distance of the listed excess
+    // nodes once all of them are reached (every value taken is ≥ the final one)
+    if (!PR && g.bound && blockIdx.x == 0 && threadIdx.x < WAVE && !done && (dense || any)) {
+        const int nb = g.ctl->n_bx;
+        if (nb > 0 && nb <= BX_CAP) {
+            long long d = 0;
+            if ((int)threadIdx.x < nb) d = atom_load(&g.dist[ni(g.bx[threadIdx.x])]);
+            d = wave_max(d);
+            if (threadIdx.x == 0 && d < INF64)
+                __hip_atomic_fetch_min(&g.ctl->bf_bound, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     scans = wave_sum(scans);
@@ -1802,17 +1843,32 @@ __device__ __forceinline__ void clear_fronts(const DG& g, const Front* fs) {
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) fs[0].hub[h] = fs[1].hub[h] = fs[2].hub[h] = 0;
 }
 
+// Wave-aggregated append of the lanes with on set to the bound's excess list.
+__device__ __forceinline__ void bx_append(const DG& g, bool on, int v) {
+    const unsigned long long m = __ballot(on);
+    if (!m) return;
+    int base = 0;
+    if (lane_id() == 0) base = atomicAdd(&g.ctl->n_bx, (int)__popcll(m));
+    base = __shfl(base, 0);
+    if (on) {
+        const int idx = base + (int)__popcll(m & ((1ULL << lane_id()) - 1));
+        if (idx < BX_CAP) g.bx[idx] = v;
+    }
+}
+
 // GU init: drain hub inboxes, dist = 0 at deficits / INF elsewhere, clean flags.
 // A cycle whose predecessor left its update unconverged (gu_pending) continues
 // that update instead; seq0 = the sequence number of this cycle's first round.
 // The deficits are the first round's frontier (a sparse round: the dense pass
 // over every node cost 16–60 µs per update). Each flag is set by the thread that
 // cleared it (same grid-stride mapping as clear_fronts; hubs: block 0).
-__global__ void k_gu_init(DG g, int seq0) {
+__global__ void k_gu_init(DG g, int seq0, int list) {
     if (g.ctl->gu_pending) return;
     clear_fronts(g, g.bf);
     const Front F0 = g.bf[seq0 % 3];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&g.ctl->bf_bound, INF64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g.ctl->gu_B = INF64;
         g.ctl->bf_done = 0;
         g.ctl->gu_L = 0;
         g.ctl->bf_r0 = g.ctl->bf_count;
@@ -1822,17 +1878,29 @@ __global__ void k_gu_init(DG g, int seq0) {
         g.ctl->aug_short = 0;
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = k == seq0 % 3 ? 1 : 0;
     }
-    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.hub_base; v += (long long)gridDim.x * BLK) {
-        const long long e = atom_load(&g.excess[v]);
-        g.dist[ni(v)] = e < 0 ? 0 : INF64;
-        if (e < 0) F0.flag[v] = 1;
+    // list: the host expects few excess nodes (the last apply found ≤ BX_CAP) —
+    // list them (n_bx, reset by k_gu_max) so the rounds can bound the update
+    for (long long v0 = blockIdx.x * (long long)BLK; v0 < g.hub_base; v0 += (long long)gridDim.x * BLK) {
+        const long long v = v0 + threadIdx.x;
+        long long e = 0;
+        if (v < g.hub_base) {
+            e = atom_load(&g.excess[v]);
+            g.dist[ni(v)] = e < 0 ? 0 : INF64;
+            if (e < 0) F0.flag[v] = 1;
+        }
+        if (list) bx_append(g, e > 0, (int)v);
     }
     if (blockIdx.x == 0)
-        for (int h = threadIdx.x; h < g.nheavy; h += BLK) {
-            drain_inbox(g, h);
-            const long long e = atom_load(&g.excess[g.hub_base + h]);
-            g.dist[ni(g.hub_base + h)] = e < 0 ? 0 : INF64;
-            if (e < 0) F0.hub[h] = 1;
+        for (int h0 = 0; h0 < g.nheavy; h0 += BLK) {
+            const int h = h0 + threadIdx.x;
+            long long e = 0;
+            if (h < g.nheavy) {
+                drain_inbox(g, h);
+                e = atom_load(&g.excess[g.hub_base + h]);
+                g.dist[ni(g.hub_base + h)] = e < 0 ? 0 : INF64;
+                if (e < 0) F0.hub[h] = 1;
+            }
+            if (list) bx_append(g, e > 0, g.hub_base + h);
         }
 }
 
@@ -1851,14 +1919,26 @@ __global__ void k_pr_init(DG g, int seq0) {
 // End of a cycle: an update that has not converged is continued by the next
 // cycle; the control block goes straight to pinned host memory (a copy engine
 // transfer would drain the queue around it: ~65 µs of idle GPU per cycle).
-__global__ void k_cycle_end(DG g, Ctl* host) {
+__global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
     static_assert(sizeof(Ctl) % 4 == 0, "Ctl is copied as words");
-    if (threadIdx.x == 0) g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;
+    if (threadIdx.x == 0) {
+        if (fwd) {
+            const int pend = (g.ctl->fs_done || g.ctl->fs_fail) ? 0 : 1;
+            g.ctl->fs_pending = pend;
+            if (!pend) g.ctl->fs_cnt[0] = g.ctl->fs_cnt[1] = g.ctl->fs_cnt[2] = 0;
+        } else {
+            g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;
+        }
+    }
     __syncthreads();
     const int* src = reinterpret_cast<const int*>(g.ctl);
     int* dst = reinterpret_cast<int*>(host);
     for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x)
         __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    // a forward init counts excess nodes into n_exc from every block: zero it here
+    // (a backward init zeroes it itself); a search still running keeps its count
+    if (threadIdx.x == 0 && !(fwd && g.ctl->fs_pending)) g.ctl->n_exc = 0;
     __threadfence_system();
 }
 
@@ -1878,6 +1958,18 @@ __global__ void k_gu_max(DG g) {
         }
     }
     if (!g.ctl->bf_done) return;
+    if (g.bound && blockIdx.x == 0 && threadIdx.x < WAVE) {
+        // a bounded update caps the prices at the listed excess nodes' largest
+        // distance (exact there; every node at or beyond it gets the cap)
+        const int nb = g.ctl->n_bx;
+        if (nb > 0 && nb <= BX_CAP) {
+            long long d = 0;
+            if ((int)threadIdx.x < nb) d = atom_load(&g.dist[ni(g.bx[threadIdx.x])]);
+            d = wave_max(d);
+            if (threadIdx.x == 0) g.ctl->gu_B = d;
+        }
+        if (threadIdx.x == 0) g.ctl->n_bx = 0;   // the next update lists afresh
+    }
     long long mx = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = atom_load(&g.dist[ni(v)]);
@@ -1900,6 +1992,7 @@ __global__ void k_gu_apply(DG g, int sseq) {
     const long long eps = g.ctl->eps;
     const long long lim = (1LL << 60) / eps;
     long long L = g.ctl->gu_L;
+    L = L < g.ctl->gu_B ? L : g.ctl->gu_B;   // bounded update: the cap
     L = L < lim ? L : lim;
     const Front F = g.sf[sseq % 3];
     int out = 0, xv = -1;
@@ -2139,6 +2232,230 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
         if (reached) atomicAdd(g.ctr + sh * NCTR + C_AUGWALK, 1ULL);
         if (hops) atomicAdd(g.ctr + sh * NCTR + C_AUGHOP, (unsigned long long)hops);
     }
+}
+
+// ------------------------------------------------- forward tail update ---
+// Once only a few nodes hold excess, a global update (Bellman-Ford from every
+// deficit over the whole graph, ~40–60 rounds) moves about one unit per cycle.
+// The forward update searches from the excess nodes instead: distances d_f
+// over residual arcs of length floor(rc/ε)+1 (≥ 0), stopping at the nearest
+// deficit's distance D, then p ← p − ε·max(0, D − d_f) — the dual step of a
+// successive-shortest-path solver. Every residual arc keeps length ≥ 0
+// (ε-optimality), and each arc of a shortest path from an excess node to a
+// deficit at distance D ends with reduced cost in [−ε, 0) (admissible), so one
+// unit per such deficit is pushed along the search's parent arcs (k_fs_trace).
+// The search touches only the nodes nearer than D (thousands, not the graph).
+// A node's key — its record's dist slot — packs d_f above the arc that set it.
+__device__ __forceinline__ long long fs_dist(long long key) { return key >> FS_PB; }
+
+// Append the lanes with on set to list l (wave-aggregated); overflow fails the search.
+__device__ __forceinline__ void fs_append(const DG& g, int l, bool on, int v) {
+    const unsigned long long m = __ballot(on);
+    if (!m) return;
+    int base = 0;
+    if (lane_id() == 0) base = atomicAdd(&g.ctl->fs_cnt[l], (int)__popcll(m));
+    base = __shfl(base, 0);
+    if (on) {
+        const int idx = base + (int)__popcll(m & ((1ULL << lane_id()) - 1));
+        if (idx < g.fl_cap) g.fl[(size_t)l * g.fl_cap + idx] = v;
+        else g.ctl->fs_fail = 1;
+    }
+}
+
+// Init: every excess node is a source (d_f 0, no parent), everything else
+// unreached; the sources are the first round's frontier. A search that did not
+// converge last cycle (fs_pending) is continued instead.
+__global__ void k_fs_init(DG g, int seq0) {
+    if (g.ctl->fs_pending) return;
+    clear_fronts(g, g.bf);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&g.ctl->fs_D, INF64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g.ctl->fs_done = 0;
+        g.ctl->fs_fail = 0;
+        g.ctl->fs_rounds = 0;
+        g.ctl->n_fdef = 0;
+        g.ctl->fs_moved = 0;   // (n_exc was reset by the last cycle's end: this kernel counts into it)
+    }
+    const int l0 = seq0 % 3;
+    for (long long v0 = blockIdx.x * (long long)BLK; v0 < g.hub_base; v0 += (long long)gridDim.x * BLK) {
+        const long long v = v0 + threadIdx.x;
+        long long e = 0;
+        if (v < g.hub_base) {
+            e = atom_load(&g.excess[v]);
+            g.dist[ni(v)] = e > 0 ? FS_NONE : INF64;
+        }
+        const unsigned long long m = __ballot(e > 0);
+        if (m && lane_id() == 0) atomicAdd(&g.ctl->n_exc, (int)__popcll(m));
+        fs_append(g, l0, e > 0, (int)v);
+    }
+    if (blockIdx.x == 0)
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) {
+            drain_inbox(g, h);
+            const long long e = atom_load(&g.excess[g.hub_base + h]);
+            g.dist[ni(g.hub_base + h)] = e > 0 ? FS_NONE : INF64;
+            if (e > 0) {
+                g.bf[l0].hub[h] = 1;
+                atomicAdd(&g.ctl->n_exc, 1);
+            }
+        }
+}
+
+// Relax residual out-arc a of u (distance du, price pu). Returns 1 when a
+// non-hub, non-deficit head w was lowered and is not yet listed for the next round.
+__device__ __forceinline__ int fs_relax(const DG& g, const Front& N, int a, long long du, long long pu, long long eps,
+                                        long long B, int& wout) {
+    const Pos q = ld_pos(g.pos + a);
+    const int w = q.head;
+    const long long pw = g.p0[ni(w)];
+    const long long kw = atom_load(&g.dist[ni(w)]);
+    const long long ew = atom_load(&g.excess[w]);
+    if (q.rcap <= 0) return 0;
+    long long len = floordiv(q.cost + pu - pw, eps) + 1;
+    len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
+    const long long cand = du + len;
+    if (cand > B || cand >= FS_DMAX || cand >= fs_dist(kw)) return 0;
+    const long long key = (cand << FS_PB) | (long long)a;
+    if (key >= atom_min_ret(&g.dist[ni(w)], key)) return 0;
+    if (ew < 0) {   // a deficit: the search's bound; paths end here
+        __hip_atomic_fetch_min(&g.ctl->fs_D, cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (w >= g.hub_base) {
+        N.hub[w - g.hub_base] = 1;
+        return 0;
+    }
+    if (N.flag[w]) return 0;
+    N.flag[w] = 1;
+    wout = w;
+    return 1;
+}
+
+// One round: the listed nodes (one wave per node, 64 arcs per batch) and the
+// flagged hubs (HSPLIT workgroups per 1024-arc chunk) relax their out-arcs.
+__global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
+    const int lin = seq % 3, lout = (seq + 1) % 3;
+    const Front F = g.bf[lin], N = g.bf[lout];
+    if (blockIdx.x == 0) {   // the buffers round seq + 1 appends to were read by round seq − 1
+        for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.bf[(seq + 2) % 3].hub[h] = 0;
+        if (threadIdx.x == 0) g.ctl->fs_cnt[(seq + 2) % 3] = 0;
+    }
+    const int done = g.ctl->fs_done | g.ctl->fs_fail;
+    const int cnt = g.ctl->fs_cnt[lin];
+    const long long B = atom_load(&g.ctl->fs_D);
+    const long long eps = g.ctl->eps;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !done) {
+        int hub_any = 0;
+        for (int h = 0; h < g.nheavy; ++h) hub_any |= F.hub[h];
+        if (cnt == 0 && !hub_any) g.ctl->fs_done = 1;   // empty frontier: converged
+        else {
+            g.ctl->fs_rounds += 1;
+            atomicAdd(g.ctr + C_BFROUND, 1ULL);
+        }
+    }
+    if (done) return;
+    const int nhb = g.nhitems * HSPLIT;
+    const int lane = lane_id();
+    if ((int)blockIdx.x < nhb) {
+        const HItem it = g.hitems[blockIdx.x / HSPLIT];
+        if (!F.hub[it.hid]) return;
+        const long long du = fs_dist(atom_load(&g.dist[ni(it.node)]));
+        const long long pu = g.p0[ni(it.node)];
+        const int sub = (int)blockIdx.x % HSPLIT;
+        for (int k = 0; k < BF_PER_T; ++k) {
+            const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
+            int w = -1;
+            const int add = a < it.end ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            fs_append(g, lout, add, w);
+        }
+        return;
+    }
+    const int nw = ((int)gridDim.x - nhb) * WPB;
+    for (int i = ((int)blockIdx.x - nhb) * WPB + (int)(threadIdx.x >> 6); i < cnt; i += nw) {
+        const int v = g.fl[(size_t)lin * g.fl_cap + i];
+        const long long key = atom_load(&g.dist[ni(v)]);
+        const long long pu = g.p0[ni(v)];
+        const long long ev = atom_load(&g.excess[v]);
+        int b0, b1;
+        seg_of(g.p0, v, b0, b1);
+        if (lane == 0) F.flag[v] = 0;
+        if (ev < 0) continue;   // a deficit ends its paths
+        const long long du = fs_dist(key);
+        for (int base = b0; base < b1; base += WAVE) {
+            const int a = base + lane;
+            int w = -1;
+            const int add = a < b1 ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            fs_append(g, lout, add, w);
+        }
+    }
+}
+
+// Apply the dual step of a converged search: p ← p − ε·(D − d_f) below D, and
+// list the deficits found at distance D for the trace.
+__global__ void k_fs_apply(DG g) {
+    if (!g.ctl->fs_done || g.ctl->fs_fail) return;
+    const long long D = atom_load(&g.ctl->fs_D);
+    if (D >= FS_DMAX) {   // no deficit in range: a backward update decides (infeasible or not)
+        if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->fs_fail = 1;
+        return;
+    }
+    const long long eps = g.ctl->eps;
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
+        const long long d = fs_dist(atom_load(&g.dist[ni(v)]));
+        if (d < D) {
+            const long long np = g.p0[ni(v)] - eps * (D - d);
+            g.p0[ni(v)] = np;
+            g.p1[ni(v)] = np;
+        } else if (d == D && atom_load(&g.excess[v]) < 0) {
+            const int idx = atomicAdd(&g.ctl->n_fdef, 1);
+            if (idx < FDEF_CAP) g.fdef[idx] = (int)v;
+        }
+    }
+}
+
+// Trace: one unit (or the path's bottleneck) from each listed deficit back along
+// the parent arcs to its excess node, one deficit after another in one thread
+// (pass 1 checks every arc is residual and admissible under the updated prices
+// and finds the amount; pass 2 pushes). A path that fails the check is skipped.
+__global__ void k_fs_trace(DG g) {
+    if (threadIdx.x != 0) return;
+    if (!g.ctl->fs_done || g.ctl->fs_fail) return;
+    const int nd = min(g.ctl->n_fdef, FDEF_CAP);
+    int moved = 0;
+    for (int k = 0; k < nd; ++k) {
+        const int t = g.fdef[k];
+        long long amt = -atom_load(&g.excess[t]);
+        int v = t, src = -1;
+        for (int hops = 0; hops < 4096 && amt > 0; ++hops) {
+            const long long key = atom_load(&g.dist[ni(v)]);
+            const long long a = key & FS_NONE;
+            if (a == FS_NONE) {
+                src = v;
+                break;
+            }
+            const Pos q = ld_pos(g.pos + a);
+            const long long r = atom_load(&g.pos[a].rcap);
+            const int u = g.pos[q.rev].head;
+            if (r <= 0 || q.cost + g.p0[ni(u)] - g.p0[ni(v)] >= 0) break;
+            amt = r < amt ? r : amt;
+            v = u;
+        }
+        if (src < 0 || src == t) continue;
+        const long long es = atom_load(&g.excess[src]);
+        amt = es < amt ? es : amt;
+        if (amt <= 0) continue;
+        v = t;
+        while (v != src) {
+            const long long a = atom_load(&g.dist[ni(v)]) & FS_NONE;
+            const int rv = g.pos[a].rev;
+            atom_add(&g.pos[a].rcap, -amt);
+            atom_add(&g.pos[rv].rcap, amt);
+            v = g.pos[rv].head;
+        }
+        atom_add(&g.excess[src], -amt);
+        atom_add(&g.excess[t], amt);
+        ++moved;
+    }
+    g.ctl->fs_moved = moved;
 }
 
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
@@ -2560,6 +2877,8 @@ struct EngineImpl {
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
     DBuf<int> xl, xl2;                 // walker start nodes (k_augment)
+    DBuf<int> bx;                      // excess nodes of the running update (distance bound)
+    DBuf<int> fl, fdef;                // forward tail update: frontier lists, traced deficits
     DBuf<long long> aug_req;           // per hub claim counter (k_aug_hub)
     DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
@@ -2627,7 +2946,7 @@ struct EngineImpl {
         for (auto& b : cls_list) b.release();
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
         q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
-        flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
+        flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); bx.release(); fl.release(); fdef.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
@@ -2714,6 +3033,10 @@ struct EngineImpl {
         g.hnchunks = hnchunks.p;
         g.xl = xl.p;
         g.xl2 = xl2.p;
+        g.bx = bx.p;
+        g.fl = fl.p;
+        g.fl_cap = (int)(fl.n / 3);
+        g.fdef = fdef.p;
         g.aug_req = aug_req.p;
         g.q_req = q_req.p;
         g.q_taken = q_taken.p;
@@ -2786,6 +3109,8 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     KS_CHECK(s.ctr.ensure(CTR_SHARDS * NCTR));
     KS_CHECK(s.xl.ensure(AUG_KMAX));
     KS_CHECK(s.xl2.ensure(AUG_K2));
+    KS_CHECK(s.bx.ensure(BX_CAP));
+    KS_CHECK(s.fdef.ensure(FDEF_CAP));
     KS_CHECK(s.sctl.ensure(1));
     KS_CHECK(hipMemset(s.sctl.p, 0, sizeof(StoreCtl)));
     KS_CHECK(hipHostMalloc(&s.h_ctl, sizeof(Ctl)));
@@ -3129,6 +3454,7 @@ static int build(EngineImpl& s, std::string& err) {
         KS_CHECK(s.hnchunks.ensure(s.nheavy));
         KS_CHECK(s.inbox.ensure((size_t)s.nheavy * SHARDS));
         KS_CHECK(s.flags.ensure(6 * (size_t)std::max(1, s.hub_base)));
+        KS_CHECK(s.fl.ensure(3 * ((size_t)std::max(1, s.nn) + 4096)));
         KS_CHECK(s.hubflags.ensure(6 * (size_t)std::max(1, s.nheavy)));
         KS_CHECK(hipMemsetAsync(s.flags.p, 0, 6 * (size_t)std::max(1, s.hub_base), st));
         KS_CHECK(hipMemsetAsync(s.hubflags.p, 0, 6 * (size_t)std::max(1, s.nheavy) * sizeof(int), st));
@@ -3642,12 +3968,20 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const ks_opts& o = s.opts;
     DG g = s.dg();
     g.expand = o.two_hop < 0 ? 0 : 1;      // two hops per round through tasks and PUs
+    g.bound = o.bf_bound < 0 ? 0 : 1;      // tail updates bounded at the excess nodes' distances
     g.aug_k = o.tail_nodes > 0 ? std::min(AUG_KMAX, (int)o.tail_nodes) : 64;
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
     const int sgrid = s.sparse_grid();     // sparse Bellman-Ford rounds
     const int wgrid = s.sweep_grid();      // sweeps
     const int ngrid = grid_for(nn, 2048);
+    const int fsgrid = s.nhitems * HSPLIT + FS_LIST_BLOCKS;   // forward tail rounds
+    // forward tail updates once ≤ fwd_k nodes hold excess (ks_opts.fwd_nodes; the
+    // search key packs an arc position into FS_PB bits)
+    const bool use_fwd = o.fwd_nodes > 0 && s.m2cap < FS_NONE;   // off by default
+    const int fwd_k = (int)o.fwd_nodes;
+    int kf = 16;                        // forward rounds enqueued per cycle (adaptive)
+    uint64_t fwd_updates = 0;
     const int alpha = o.alpha >= 2 ? o.alpha : 8;
     int gi_base = o.gu_interval > 0 ? o.gu_interval : 24;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
@@ -3761,11 +4095,31 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         uint64_t phase_sweeps = 0;
         int gi = gi_base;     // sweeps in the next cycle (fewer in a phase's tail, where walks augment)
         int phase_peak = 0;   // most excess nodes seen by an update of this phase
+        int list = 0;         // the next update lists its excess nodes for the bound (the last apply found ≤ BX_CAP)
+        int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
+        int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
         int rc = KS_OK;
+        // Forward cycle: [init (or continue the pending search)][kf rounds][apply]
+        // [trace][end]; no sweeps (the trace routes the units).
+        auto enqueue_fwd = [&](int par) -> hipError_t {
+            hipLaunchKernelGGL(k_fs_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+            for (int r = 0; r < kf; ++r) {
+                hipLaunchKernelGGL(k_fs_round, dim3(fsgrid), dim3(BLK), 0, st, g, bseq);
+                ++bseq;
+                ++bf_launches;
+            }
+            hipError_t e = hipEventRecord(s.cev[par][0], st);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
+            if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_fs_trace, dim3(1), dim3(WAVE), 0, st, g);
+            hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
+            return hipEventRecord(s.cdone[par], st);
+        };
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
-            hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+            hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, list);
             for (int r = 0; r < kb; ++r) {   // sparse from the first round: k_gu_init flags the deficits
                 hipLaunchKernelGGL(k_bf_round<false>, dim3(sgrid), dim3(BLK), 0, st, g, bseq, 0);
                 ++bseq;
@@ -3785,7 +4139,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
             }
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
-            hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par]);
+            hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 0);
             sseq += gi;
             return hipEventRecord(s.cdone[par], st);
         };
@@ -3798,6 +4152,43 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         hipEvent_t prev_end = s.cstart;
         int cur = 0;
         for (;;) {
+            if (fwd) {
+                KS_CHECK(enqueue_fwd(cur));
+                KS_CHECK(hipEventSynchronize(s.cdone[cur]));
+                const Ctl* hc = s.h_cyc[cur];
+                const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][1], s.cdone[cur]);
+                ms_bf_k += t_bf;
+                ms_sw_k += t_sw;
+                prev_end = s.cdone[cur];
+                cur ^= 1;
+                if (cycle_log)
+                    std::fprintf(stderr, "fwd cycle phase %d eps %lld rounds %d bf_ms %.3f tr_ms %.3f n_exc %d done %d fail %d D %lld deficits %d moved %d\n",
+                                 phases, eps_ph, hc->fs_rounds, t_bf, t_sw, hc->n_exc, hc->fs_done, hc->fs_fail,
+                                 hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef, hc->fs_moved);
+                if (hc->n_exc == 0) break;   // no excess left: the phase is done
+                if (hc->fs_fail) {           // (list overflow, or no deficit in range)
+                    fwd = 0;
+                    fwd_block = 1;
+                    continue;
+                }
+                if (!hc->fs_done) {          // the search continues next cycle
+                    kf = std::min(256, kf * 2);
+                    continue;
+                }
+                ++gus;
+                ++fwd_updates;
+                kf = std::max(8, std::min(256, hc->fs_rounds + 4));
+                if (hc->fs_moved == 0) {
+                    fwd = 0;
+                    fwd_block = 1;
+                }
+                if (wall_s() > kSolveWallLimitS) {
+                    (void)hipStreamSynchronize(st);
+                    err = "forward tail did not converge (" + std::to_string(wall_s()) + " s)";
+                    return KS_E_DEVICE;
+                }
+                continue;
+            }
             KS_CHECK(enqueue(cur));
             KS_CHECK(hipEventSynchronize(s.cdone[cur]));
             const Ctl* hc = s.h_cyc[cur];
@@ -3880,6 +4271,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 break;   // a coarse phase: the next one absorbs the few units left
             }
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
+            list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
+            fwd = use_fwd && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
+            fwd_block = 0;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
                 err = "push/relabel did not converge (sweeps " + std::to_string(phase_sweeps) + ", " +
@@ -3943,8 +4337,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     } while (eps > 1);
 
     if (cycle_log)
-        std::fprintf(stderr, "solve phases %d updates %llu early phase ends %llu\n", phases, (unsigned long long)gus,
-                     (unsigned long long)early_exits);
+        std::fprintf(stderr, "solve phases %d updates %llu (forward %llu) early phase ends %llu\n", phases,
+                     (unsigned long long)gus, (unsigned long long)fwd_updates, (unsigned long long)early_exits);
     if (status == KS_E_INFEASIBLE)
         err = "infeasible: some supply cannot reach a demand node (code " + std::to_string(s.h_ctl->infeasible) +
               ", phase " + std::to_string(phases) + ", eps " + std::to_string(eps) + ", updates " +

@@ -51,7 +51,8 @@ class KsOpts(C.Structure):
                 ("phase_exit", C.c_int32), ("phase_frac", C.c_int32), ("tail_sweeps", C.c_int32),
                 ("bf_margin", C.c_int32), ("two_hop", C.c_int32), ("log_cycles", C.c_int32),
                 ("fault_inject", C.c_int32), ("walk_passes", C.c_int32), ("tail_nodes", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class KsResult(C.Structure):

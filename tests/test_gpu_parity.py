@@ -295,6 +295,26 @@ def test_tail_walks_do_not_change_the_optimum(opts):
                 solve_and_check(c2, g, c, fv)
 
 
+@pytest.mark.parametrize("opts", [{"fwd_nodes": 4}, {"fwd_nodes": 64}, {"fwd_nodes": 4096, "tail_nodes": 4096},
+                                  {"bf_bound": -1}, {"fwd_nodes": 16, "price_refine": 0}])
+def test_tail_updates_do_not_change_the_optimum(opts):
+    """The tail's update kinds: the forward update (a search from the
+    excess nodes to the nearest deficit, pushes along its shortest paths) off,
+    from 64 excess nodes, from any count (every cycle once a phase is in its
+    tail), and down to ε = 1 without price refinement; the bounded global update
+    off. Same optimum as the oracle, flow re-verified, on a config-2-sized cell
+    and random graphs (several deficits, lower bounds, parallel paths)."""
+    with native.Context(0, **opts) as c2:
+        g = gen.quincy(10_000, 1_000, 25, 100, 2)
+        st, c, fv, _, _ = ko.ssp(g)
+        assert st == 0
+        solve_and_check(c2, g, c, fv)
+        for trial, g in random_graphs(4242, 15):
+            st, c, fv, _, _ = ko.ssp(g)
+            if st == 0:
+                solve_and_check(c2, g, c, fv)
+
+
 @pytest.mark.parametrize("fault", [1, 2])
 def test_failed_certificate_is_recovered(fault):
     """A failed final optimality certificate is repaired, not fatal

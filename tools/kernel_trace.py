@@ -57,6 +57,29 @@ def main():
                 cur = []
             elif k == "k_bf_round<false>" and d >= 3:
                 cur.append(d)
+    if "--cycles" in sys.argv:   # one line per cycle: span, host gap before it, device time by kernel kind
+        kinds = {"k_bf_round<false>": "bf", "k_sweep": "sw", "k_augment": "aug", "k_aug_hub": "hub"}
+        starts = [i for i, k in enumerate(names) if k == "k_gu_init"]
+        print("cycle span_us host_gap_us bf_n bf_us bf_work_n sw_us aug_us other_us idle_us")
+        for c, i0 in enumerate(starts):
+            i1 = starts[c + 1] if c + 1 < len(starts) else len(names)
+            ends = [j for j in range(i0, i1) if names[j] == "k_cycle_end"]
+            if not ends:
+                continue
+            j1 = ends[0] + 1
+            span = (en[j1 - 1] - st[i0]) / 1e3
+            hgap = (st[i0] - en[i0 - 1]) / 1e3 if i0 > 0 else 0.0
+            acc = {"bf": 0.0, "sw": 0.0, "aug": 0.0, "hub": 0.0, "other": 0.0}
+            nbf = nbfw = 0
+            for j in range(i0, j1):
+                kd = kinds.get(names[j], "other")
+                acc[kd] += dur[j]
+                if kd == "bf":
+                    nbf += 1
+                    nbfw += dur[j] >= 3
+            busy = sum(acc.values())
+            print(f"{c} {span:.0f} {hgap:.0f} {nbf} {acc['bf']:.0f} {nbfw} {acc['sw']:.0f} "
+                  f"{acc['aug'] + acc['hub']:.0f} {acc['other']:.0f} {span - busy:.0f}")
     print(f"gaps: n={len(gaps)} sum={gaps.sum() / 1e3:.2f} ms p50={np.median(gaps):.2f} p90={np.percentile(gaps, 90):.2f} us")
 
 
