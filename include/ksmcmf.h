@@ -125,8 +125,10 @@ typedef struct ks_opts {
                                   those nodes and caps prices there [on]; < 0 off       */
     int32_t  fwd_nodes;        /* once ≤ fwd_nodes nodes hold excess, a cycle searches
                                   from them to the nearest deficit and pushes along the
-                                  search's shortest paths instead of a global update
-                                  [0 = off]                                             */
+                                  search's shortest paths instead of a global update;
+                                  a search that takes more than half the rounds of the
+                                  last global update, or a cycle more than half its time,
+                                  ends them for the phase [64]; < 0 off                 */
     int32_t  reserved[4];
 } ks_opts;
 

@@ -109,6 +109,11 @@ constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess nod
 constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
+#ifdef KS_FWD_NOADAPT
+#define KS_FWD_FIXED 1
+#else
+#define KS_FWD_FIXED 0
+#endif
 
 struct Ctl {
     long long eps;
@@ -141,6 +146,8 @@ struct Ctl {
     int fs_rounds;         // rounds of the running search that had a frontier
     int n_fdef;            // deficits at distance D listed for the trace
     int fs_moved;          // units the trace moved
+    long long u_exc;       // excess units the last apply (backward) / init (forward) found
+    int fs_maxcnt;         // the running search's widest frontier (nodes; hubs count 1024 each)
 };
 
 struct HItem {
@@ -199,6 +206,7 @@ struct DG {
     int* bx;               // excess nodes of the running update (the first BX_CAP; k_gu_init)
     int* fl;               // forward search: 3 rotating frontier lists of fl_cap node ids
     int fl_cap;
+    int fs_wide;           // a forward frontier wider than this fails its search as wide
     int* fdef;             // forward search: deficits at the found distance (FDEF_CAP)
     int bound;             // 1: prune Bellman-Ford offers at ctl->bf_bound (ks_opts.bf_bound >= 0)
     long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
@@ -1874,6 +1882,7 @@ __global__ void k_gu_init(DG g, int seq0, int list) {
         g.ctl->bf_r0 = g.ctl->bf_count;
         g.ctl->bf_seq0 = seq0;
         g.ctl->n_exc = 0;
+        g.ctl->u_exc = 0;
         g.ctl->aug_reached = 0;
         g.ctl->aug_short = 0;
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = k == seq0 % 3 ? 1 : 0;
@@ -1938,7 +1947,10 @@ __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
     __syncthreads();
     // a forward init counts excess nodes into n_exc from every block: zero it here
     // (a backward init zeroes it itself); a search still running keeps its count
-    if (threadIdx.x == 0 && !(fwd && g.ctl->fs_pending)) g.ctl->n_exc = 0;
+    if (threadIdx.x == 0 && !(fwd && g.ctl->fs_pending)) {
+        g.ctl->n_exc = 0;
+        g.ctl->u_exc = 0;
+    }
     __threadfence_system();
 }
 
@@ -1996,9 +2008,11 @@ __global__ void k_gu_apply(DG g, int sseq) {
     L = L < lim ? L : lim;
     const Front F = g.sf[sseq % 3];
     int out = 0, xv = -1;
+    long long units = 0;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = atom_load(&g.dist[ni(v)]);
         const long long e = atom_load(&g.excess[v]);
+        units += e > 0 ? e : 0;
         if (d >= INF64 && e > 0) atomicOr(&g.ctl->infeasible, 8);
         const long long dd = d < L ? d : L;
         const long long np = g.p0[ni(v)] - eps * dd;
@@ -2017,6 +2031,8 @@ __global__ void k_gu_apply(DG g, int sseq) {
         base = atomicAdd(&g.ctl->n_exc, (int)__popcll(ex));
     }
     base = __shfl(base, 0);
+    units = wave_sum(units);
+    if (units && lane_id() == 0) atom_add(&g.ctl->u_exc, units);
     if (out) {
         const int idx = base + (int)__popcll(ex & ((1ULL << lane_id()) - 1));
         if (idx < g.aug_k) g.xl[idx] = xv;
@@ -2275,6 +2291,7 @@ __global__ void k_fs_init(DG g, int seq0) {
         g.ctl->fs_rounds = 0;
         g.ctl->n_fdef = 0;
         g.ctl->fs_moved = 0;   // (n_exc was reset by the last cycle's end: this kernel counts into it)
+        g.ctl->fs_maxcnt = 0;
     }
     const int l0 = seq0 % 3;
     for (long long v0 = blockIdx.x * (long long)BLK; v0 < g.hub_base; v0 += (long long)gridDim.x * BLK) {
@@ -2286,6 +2303,8 @@ __global__ void k_fs_init(DG g, int seq0) {
         }
         const unsigned long long m = __ballot(e > 0);
         if (m && lane_id() == 0) atomicAdd(&g.ctl->n_exc, (int)__popcll(m));
+        const long long units = wave_sum(e > 0 ? e : 0);
+        if (units && lane_id() == 0) atom_add(&g.ctl->u_exc, units);
         fs_append(g, l0, e > 0, (int)v);
     }
     if (blockIdx.x == 0)
@@ -2296,6 +2315,7 @@ __global__ void k_fs_init(DG g, int seq0) {
             if (e > 0) {
                 g.bf[l0].hub[h] = 1;
                 atomicAdd(&g.ctl->n_exc, 1);
+                atom_add(&g.ctl->u_exc, e);
             }
         }
 }
@@ -2345,11 +2365,16 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
     const long long eps = g.ctl->eps;
     if (blockIdx.x == 0 && threadIdx.x == 0 && !done) {
         int hub_any = 0;
-        for (int h = 0; h < g.nheavy; ++h) hub_any |= F.hub[h];
+        for (int h = 0; h < g.nheavy; ++h) hub_any += F.hub[h];
         if (cnt == 0 && !hub_any) g.ctl->fs_done = 1;   // empty frontier: converged
         else {
             g.ctl->fs_rounds += 1;
             atomicAdd(g.ctr + C_BFROUND, 1ULL);
+            const int width = cnt + 1024 * hub_any;
+            if (width > g.ctl->fs_maxcnt) g.ctl->fs_maxcnt = width;
+            // a frontier this wide (a hub's arcs in reach) costs more per unit than
+            // the global update it replaces: fail the search as wide
+            if (width > g.fs_wide && !KS_FWD_FIXED) g.ctl->fs_fail = 2;
         }
     }
     if (done) return;
@@ -3969,6 +3994,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     DG g = s.dg();
     g.expand = o.two_hop < 0 ? 0 : 1;      // two hops per round through tasks and PUs
     g.bound = o.bf_bound < 0 ? 0 : 1;      // tail updates bounded at the excess nodes' distances
+    g.fs_wide = std::max(2048, nn / 4);   // (measured: config 4's searches ≤ nn/6 wide, config 3's hub-bound ones ~nn/4 to 3nn/4)
     g.aug_k = o.tail_nodes > 0 ? std::min(AUG_KMAX, (int)o.tail_nodes) : 64;
     const int fgrid = s.window_grid();     // dense passes over every window (saturate)
     const int dgrid = s.dense_grid();      // dense Bellman-Ford round
@@ -3978,8 +4004,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int fsgrid = s.nhitems * HSPLIT + FS_LIST_BLOCKS;   // forward tail rounds
     // forward tail updates once ≤ fwd_k nodes hold excess (ks_opts.fwd_nodes; the
     // search key packs an arc position into FS_PB bits)
-    const bool use_fwd = o.fwd_nodes > 0 && s.m2cap < FS_NONE;   // off by default
-    const int fwd_k = (int)o.fwd_nodes;
+    const bool use_fwd = o.fwd_nodes >= 0 && s.m2cap < FS_NONE;
+    const int fwd_k = o.fwd_nodes > 0 ? (int)o.fwd_nodes : 64;
     int kf = 16;                        // forward rounds enqueued per cycle (adaptive)
     uint64_t fwd_updates = 0;
     const int alpha = o.alpha >= 2 ? o.alpha : 8;
@@ -4098,6 +4124,34 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int list = 0;         // the next update lists its excess nodes for the bound (the last apply found ≤ BX_CAP)
         int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
+        bool fwd_off = false; // a forward search ran past its round budget: backward updates for the rest of the phase
+        int fs_used = 0;      // rounds enqueued for the running forward search
+        int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
+        // tail progress per mode (excess units routed per ms of device time): once the
+        // last phase's forward updates route fewer than a quarter of the units per ms
+        // the global updates did (measured: the first tail cycle of a phase routes
+        // several times the later ones' rate), it goes back to global updates
+        double rate_ms[2] = {0, 0};
+        long long rate_units[2] = {0, 0};
+        int rate_n[2] = {0, 0};
+        int last_mode = -1;   // mode of the last completed tail cycle (0 backward, 1 forward)
+        double last_ms = 0, acc_ms = 0;
+        long long last_units = 0;
+        // account a completed cycle that found `units` excess units at its start
+        auto account = [&](int mode, bool tail, double ms, long long units) {
+            if (last_mode >= 0) {
+                rate_ms[last_mode] += last_ms;
+                rate_units[last_mode] += std::max(0LL, last_units - units);
+                rate_n[last_mode] += 1;
+            }
+            last_mode = tail ? mode : -1;
+            last_ms = ms;
+            last_units = units;
+        };
+        auto fwd_worse = [&]() {
+            return !may_end_early && rate_n[1] >= 1 && rate_n[0] >= 1 && rate_ms[1] > 0 && rate_ms[0] > 0 &&
+                   4.0 * (double)rate_units[1] / rate_ms[1] < (double)rate_units[0] / rate_ms[0];
+        };
         int rc = KS_OK;
         // Forward cycle: [init (or continue the pending search)][kf rounds][apply]
         // [trace][end]; no sweeps (the trace routes the units).
@@ -4161,23 +4215,48 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 ms_sw_k += t_sw;
                 prev_end = s.cdone[cur];
                 cur ^= 1;
+                fs_used += kf;
+                acc_ms += t_bf + t_sw;
                 if (cycle_log)
-                    std::fprintf(stderr, "fwd cycle phase %d eps %lld rounds %d bf_ms %.3f tr_ms %.3f n_exc %d done %d fail %d D %lld deficits %d moved %d\n",
-                                 phases, eps_ph, hc->fs_rounds, t_bf, t_sw, hc->n_exc, hc->fs_done, hc->fs_fail,
-                                 hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef, hc->fs_moved);
+                    std::fprintf(stderr, "fwd cycle phase %d eps %lld rounds %d bf_ms %.3f tr_ms %.3f units %lld n_exc %d done %d fail %d D %lld deficits %d moved %d width %d\n",
+                                 phases, eps_ph, hc->fs_rounds, t_bf, t_sw, hc->u_exc, hc->n_exc, hc->fs_done, hc->fs_fail,
+                                 hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef, hc->fs_moved, hc->fs_maxcnt);
                 if (hc->n_exc == 0) break;   // no excess left: the phase is done
-                if (hc->fs_fail) {           // (list overflow, or no deficit in range)
+                const bool completed = hc->fs_done || hc->fs_fail || fs_used >= fwd_budget;
+                if (completed) {
+                    account(1, true, acc_ms, hc->u_exc);
+                    acc_ms = 0;
+                }
+                bool wide = hc->fs_fail == 2;
+                if (!hc->fs_fail && !hc->fs_done && fs_used >= fwd_budget && !KS_FWD_FIXED) {
+                    // longer than two global updates: drop it like a wide one
+                    KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
+                    KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
+                    wide = true;
+                }
+                if (hc->fs_fail || wide) {
+                    // list overflow or no deficit in range: one global update; a wide search
+                    // (a hub's arcs in reach: a forward update then costs more per unit than
+                    // a global one): global updates for the rest of the phase
                     fwd = 0;
                     fwd_block = 1;
+                    fwd_off = fwd_off || wide;
+                    fs_used = 0;
                     continue;
                 }
                 if (!hc->fs_done) {          // the search continues next cycle
-                    kf = std::min(256, kf * 2);
+                    kf = std::min(256, 2 * kf);
                     continue;
                 }
+                fs_used = 0;
                 ++gus;
                 ++fwd_updates;
                 kf = std::max(8, std::min(256, hc->fs_rounds + 4));
+                if (!KS_FWD_FIXED && fwd_worse()) {
+                    fwd = 0;
+                    fwd_off = true;
+                    continue;
+                }
                 if (hc->fs_moved == 0) {
                     fwd = 0;
                     fwd_block = 1;
@@ -4197,6 +4276,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             ms_bf_k += t_bf;   // init + BF rounds
             ms_sw_k += t_sw;   // sweeps + cycle end
             prev_end = s.cdone[cur];
+            acc_ms += t_bf + t_sw;
             if (hc->infeasible) {
                 rc = KS_E_INFEASIBLE;
                 std::memcpy(s.h_ctl, hc, sizeof(Ctl));
@@ -4209,8 +4289,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 continue;
             }
             if (cycle_log) {
-                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d n_exc %d walks %d/%d",
-                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->n_exc,
+                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d units %lld n_exc %d walks %d/%d",
+                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->u_exc, hc->n_exc,
                              hc->aug_reached, hc->aug_short);
                 for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
                     const int x = hc->dbg_x[k];
@@ -4253,7 +4333,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
             }
 #endif
+            account(0, hc->n_exc <= fwd_k, acc_ms, hc->u_exc);
+            acc_ms = 0;
             kb = std::max(kb_min, std::min(256, hc->bf_count - hc->bf_r0 + kb_margin));
+            fwd_budget = std::max(16, 2 * (hc->bf_count - hc->bf_r0));
             ++gus;
             sweeps += gi;
             sweep_launches += gi;
@@ -4272,7 +4355,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
-            fwd = use_fwd && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
+            fwd = use_fwd && !fwd_off && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
             fwd_block = 0;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);

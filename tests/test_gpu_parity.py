@@ -295,7 +295,7 @@ def test_tail_walks_do_not_change_the_optimum(opts):
                 solve_and_check(c2, g, c, fv)
 
 
-@pytest.mark.parametrize("opts", [{"fwd_nodes": 4}, {"fwd_nodes": 64}, {"fwd_nodes": 4096, "tail_nodes": 4096},
+@pytest.mark.parametrize("opts", [{"fwd_nodes": -1}, {"fwd_nodes": 64}, {"fwd_nodes": 4096, "tail_nodes": 4096},
                                   {"bf_bound": -1}, {"fwd_nodes": 16, "price_refine": 0}])
 def test_tail_updates_do_not_change_the_optimum(opts):
     """The tail's update kinds: the forward update (a search from the
