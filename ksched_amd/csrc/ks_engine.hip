@@ -109,6 +109,13 @@ constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess nod
 constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
+#ifndef KS_FWD_LAST
+#define KS_FWD_LAST 0              // 1: forward updates in the last phase too (guarded by the rate rule)
+#endif
+#ifndef KS_FWD_EXIT
+#define KS_FWD_EXIT 0              // 1: coarse phases in forward mode end by the global-update rule
+                                   // (measured: draining them is what makes config 4's last phase short)
+#endif
 #ifdef KS_FWD_NOADAPT
 #define KS_FWD_FIXED 1
 #else
@@ -207,6 +214,7 @@ struct DG {
     int* fl;               // forward search: 3 rotating frontier lists of fl_cap node ids
     int fl_cap;
     int fs_wide;           // a forward frontier wider than this fails its search as wide
+    int npos;              // residual positions (m2cap)
     int* fdef;             // forward search: deficits at the found distance (FDEF_CAP)
     int bound;             // 1: prune Bellman-Ford offers at ctl->bf_bound (ks_opts.bf_bound >= 0)
     long long* aug_req;    // per hub: excess claimed by its k_aug_hub chunks
@@ -2438,49 +2446,102 @@ __global__ void k_fs_apply(DG g) {
 }
 
 // Trace: one unit (or the path's bottleneck) from each listed deficit back along
-// the parent arcs to its excess node, one deficit after another in one thread
-// (pass 1 checks every arc is residual and admissible under the updated prices
-// and finds the amount; pass 2 pushes). A path that fails the check is skipped.
-__global__ void k_fs_trace(DG g) {
-    if (threadIdx.x != 0) return;
+// the parent arcs to its excess node — one wave per deficit, all in parallel.
+// Lane 0 walks the parents (each arc must end at the node it was reached from,
+// be residual, and be admissible under the updated prices) into an LDS path;
+// the wave then claims the source's excess with a CAS and every arc of the path
+// at once (one lane per arc, CAS against the residual); if any arc is short
+// (another wave took it) every claim is rolled back and the unit waits for the
+// next update. Then the reverse residuals and the deficit are credited.
+constexpr int FS_PATH = 512;       // hops a trace may take
+__global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
+    __shared__ int path[FS_PATH];
+    __shared__ int s_len, s_src;
+    __shared__ long long s_amt;
     if (!g.ctl->fs_done || g.ctl->fs_fail) return;
-    const int nd = min(g.ctl->n_fdef, FDEF_CAP);
-    int moved = 0;
-    for (int k = 0; k < nd; ++k) {
-        const int t = g.fdef[k];
+    if ((int)blockIdx.x >= min(g.ctl->n_fdef, FDEF_CAP)) return;
+    const int lane = threadIdx.x;
+    const int t = g.fdef[blockIdx.x];
+    if (lane == 0) {
         long long amt = -atom_load(&g.excess[t]);
-        int v = t, src = -1;
-        for (int hops = 0; hops < 4096 && amt > 0; ++hops) {
+        int v = t, src = -1, len = 0;
+        while (amt > 0 && len < FS_PATH) {
             const long long key = atom_load(&g.dist[ni(v)]);
             const long long a = key & FS_NONE;
             if (a == FS_NONE) {
                 src = v;
                 break;
             }
+            if (a >= g.npos) break;   // (a key not written by this search)
             const Pos q = ld_pos(g.pos + a);
             const long long r = atom_load(&g.pos[a].rcap);
             const int u = g.pos[q.rev].head;
-            if (r <= 0 || q.cost + g.p0[ni(u)] - g.p0[ni(v)] >= 0) break;
+            if (q.head != v || r <= 0 || q.cost + g.p0[ni(u)] - g.p0[ni(v)] >= 0) break;
             amt = r < amt ? r : amt;
+            path[len++] = (int)a;
             v = u;
         }
-        if (src < 0 || src == t) continue;
-        const long long es = atom_load(&g.excess[src]);
-        amt = es < amt ? es : amt;
-        if (amt <= 0) continue;
-        v = t;
-        while (v != src) {
-            const long long a = atom_load(&g.dist[ni(v)]) & FS_NONE;
-            const int rv = g.pos[a].rev;
-            atom_add(&g.pos[a].rcap, -amt);
-            atom_add(&g.pos[rv].rcap, amt);
-            v = g.pos[rv].head;
+        if (src >= 0 && src != t) {   // claim the source's excess
+            long long e = atom_load(&g.excess[src]);
+            for (;;) {
+                const long long take = e < amt ? e : amt;
+                if (take <= 0) {
+                    src = -1;
+                    break;
+                }
+                long long exp = e;
+                if (__hip_atomic_compare_exchange_strong(&g.excess[src], &exp, e - take, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    amt = take;
+                    break;
+                }
+                e = exp;
+            }
+        } else {
+            src = -1;
         }
-        atom_add(&g.excess[src], -amt);
-        atom_add(&g.excess[t], amt);
-        ++moved;
+        s_len = len;
+        s_src = src;
+        s_amt = amt;
     }
-    g.ctl->fs_moved = moved;
+    __syncthreads();
+    const int len = s_len, src = s_src;
+    const long long amt = s_amt;
+    if (src < 0) return;
+    // claim every arc of the path at once
+    bool ok = true;
+    unsigned long long mine = 0;   // bit i: this lane holds the claim on path[lane + 64 i]
+    for (int i = lane, k = 0; i < len; i += WAVE, ++k) {
+        long long* rc = &g.pos[path[i]].rcap;
+        long long r = atom_load(rc);
+        for (;;) {
+            if (r < amt) {
+                ok = false;
+                break;
+            }
+            long long exp = r;
+            if (__hip_atomic_compare_exchange_strong(rc, &exp, r - amt, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                mine |= 1ULL << k;
+                break;
+            }
+            r = exp;
+        }
+    }
+    const bool all = __all(ok);
+    for (int i = lane, k = 0; i < len; i += WAVE, ++k) {
+        if (!(mine >> k & 1)) continue;
+        if (all) atom_add(&g.pos[g.pos[path[i]].rev].rcap, amt);
+        else atom_add(&g.pos[path[i]].rcap, amt);   // roll back
+    }
+    if (lane == 0) {
+        if (all) {
+            atom_add(&g.excess[t], amt);
+            atomicAdd(&g.ctl->fs_moved, 1);
+        } else {
+            atom_add(&g.excess[src], amt);   // the unit stays for the next update
+        }
+    }
 }
 
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
@@ -3062,6 +3123,7 @@ struct EngineImpl {
         g.fl = fl.p;
         g.fl_cap = (int)(fl.n / 3);
         g.fdef = fdef.p;
+        g.npos = (int)m2cap;
         g.aug_req = aug_req.p;
         g.q_req = q_req.p;
         g.q_taken = q_taken.p;
@@ -4166,7 +4228,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_fs_trace, dim3(1), dim3(WAVE), 0, st, g);
+            hipLaunchKernelGGL(k_fs_trace, dim3(FDEF_CAP), dim3(WAVE), 0, st, g);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
             return hipEventRecord(s.cdone[par], st);
         };
@@ -4202,6 +4264,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // more GPU time than the host's decision gap). Timing: BF = from the
         // previous cycle's end (or the phase start) to after the BF rounds; sweeps
         // = from after the apply to the cycle's end.
+        if (use_fwd) {   // a phase never continues another phase's forward search
+            KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
+            KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
+        }
         KS_CHECK(hipEventRecord(s.cstart, st));
         hipEvent_t prev_end = s.cstart;
         int cur = 0;
@@ -4223,6 +4289,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                  hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef, hc->fs_moved, hc->fs_maxcnt);
                 if (hc->n_exc == 0) break;   // no excess left: the phase is done
                 const bool completed = hc->fs_done || hc->fs_fail || fs_used >= fwd_budget;
+                if (KS_FWD_EXIT && hc->fs_done && !hc->fs_fail && may_end_early && hc->n_exc <= phase_exit &&
+                    (long long)hc->n_exc * phase_frac <= phase_peak) {
+                    ++early_exits;   // a coarse phase ends as after a global update (the same rule)
+                    break;
+                }
                 if (completed) {
                     account(1, true, acc_ms, hc->u_exc);
                     acc_ms = 0;
@@ -4355,7 +4426,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
-            fwd = use_fwd && !fwd_off && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
+            fwd = use_fwd && (may_end_early || KS_FWD_LAST) && !fwd_off && !fwd_block && hc->n_exc > 0 &&
+                  hc->n_exc <= fwd_k;
             fwd_block = 0;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);

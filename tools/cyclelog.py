@@ -9,9 +9,10 @@ sys.path.insert(0, ROOT)
 from ksched_amd import churn, gen, native  # noqa: E402
 
 opts = {}
-for kv in filter(None, (sys.argv[1] if len(sys.argv) > 1 and "=" in sys.argv[1] else "").split(",")):
+for kv in filter(None, (sys.argv[1] if len(sys.argv) > 1 and "=" in sys.argv[1] and not sys.argv[1].startswith("--") else "").split(",")):
     k, v = kv.split("=")
     opts[k] = int(v)
+cfg = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--config=")), "config3")
 T, M, R, J, seed = gen.CONFIGS["config3"]
 if "--config4" in sys.argv:
     cell = churn.Cell(T, M, R, J, seed)
@@ -29,7 +30,7 @@ if "--config4" in sys.argv:
     ctx.solve()
     print("config4 round 3 graph:", ctx.solve().raw["ms"], file=sys.stderr)
 else:
-    g = gen.quincy(T, M, R, J, seed)
+    g = gen.quincy(*gen.CONFIGS[cfg])
     ctx = native.Context(0, **opts)
     ctx.load_graph(g)
     ctx.solve()
@@ -37,4 +38,4 @@ else:
     ctx = native.Context(0, log_cycles=1, **opts)
     ctx.load_graph(g)
     r = ctx.solve()
-    print("config3:", r.cost, r.raw["ms"], file=sys.stderr)
+    print(cfg + ":", r.cost, r.raw["ms"], file=sys.stderr)
