@@ -338,7 +338,7 @@ def run_incremental(args, D):
     g = cell.graph()
     ctx.load_graph(g)
     r0 = ctx.solve()
-    mp = ctx.task_mapping()
+    mp = ctx.task_mapping_arrays()
     done = arrive = T // 20
     rounds, results = [], []
     t_total = 0.0
@@ -363,7 +363,7 @@ def run_incremental(args, D):
         ta = time.perf_counter()
         r = ctx.solve()
         tb = time.perf_counter()
-        mp = ctx.task_mapping()
+        mp = ctx.task_mapping_arrays()   # ks_get_task_mapping's (task, PU) arrays: the TaskMapping
         te = time.perf_counter()
         D.sync()
         dt = D.max(time.perf_counter() - ts)

@@ -145,9 +145,10 @@ class Cell:
         return self.TASK0 + np.nonzero(self.state[:self.n_slots] == which)[0].astype(np.int64)
 
     # ---------------------------------------------------------------- rounds
-    def step(self, mapping: dict[int, int], done: int, arrive: int, age_cost: int = 10,
+    def step(self, mapping, done: int, arrive: int, age_cost: int = 10,
              seed: int | None = None) -> np.ndarray:
-        """Advance one scheduling round given the last solve's task→PU mapping;
+        """Advance one scheduling round given the last solve's task→PU mapping (a
+        dict, or the (task ids, PU ids) arrays of ks_get_task_mapping);
         returns the delta records (``DELTA_DT``) in mutation order."""
         self.round += 1
         seed = 4 + self.round if seed is None else seed
@@ -158,9 +159,16 @@ class Cell:
         old_u = self.waiting_per_job()
 
         # 1. pin the tasks the solver placed
-        if mapping:
+        if isinstance(mapping, tuple):   # (task ids, PU ids) arrays, as the C-ABI returns them
+            mapping = (np.asarray(mapping[0], np.int64), np.asarray(mapping[1], np.int64))
+        if isinstance(mapping, tuple) and mapping[0].shape[0]:
+            t, p = mapping
+        elif isinstance(mapping, dict) and mapping:
             t = np.fromiter(mapping.keys(), np.int64, len(mapping))
             p = np.fromiter(mapping.values(), np.int64, len(mapping))
+        else:
+            t = None
+        if t is not None:
             order = np.argsort(t, kind="stable")
             t, p = t[order], p[order]
             sl = t - self.TASK0

@@ -34,6 +34,8 @@ struct ks_ctx {
     int64_t dev_sink_supply = 0;           // the sink's supply as the device has it
     bool have_solution = false;
     bool flows_fresh = false;
+    bool map_fresh = false;                // map_dense holds the current solve's task→PU vector
+    std::vector<uint64_t> map_dense;       // per live task slot in slot order: its PU (0: none)
     bool store_bad = false;                // a load / apply failed on the device: reload first
     std::vector<ks_flow> flows;
 

@@ -231,6 +231,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
     c->sink_id = 0;
     for (uint64_t id = 1; id <= maxid; ++id) account(c, id, c->nodes[id], 1);
     c->have_solution = false;
+    c->map_fresh = false;
     c->flows_fresh = false;
     std::vector<int64_t> supply(maxid);
     std::vector<uint8_t> type(maxid), alive(maxid);
@@ -342,6 +343,7 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
         if (now.alive && now.type == KS_NODE_SINK) c->dev_sink_supply = now.excess;
     }
     c->have_solution = false;
+    c->map_fresh = false;
     c->flows_fresh = false;
     rc = c->eng.apply(edits.data(), edits.size(), d, k, c->nslots(), c->err);
     if (rc) {
@@ -466,6 +468,7 @@ int ks_solve(ks_ctx* c, ks_result* out) {
     ks_result r;
     std::memset(&r, 0, sizeof(r));
     c->have_solution = false;
+    c->map_fresh = false;
     c->flows_fresh = false;
     int rc = KS_OK;
     // auto-sink: the sink absorbs every other supply (its demand drifts without a
@@ -483,6 +486,7 @@ int ks_solve(ks_ctx* c, ks_result* out) {
         if (rc == KS_OK) c->dev_sink_supply = -c->sum_others;
     }
     if (rc == KS_OK) rc = c->eng.solve(r, c->opts.warm_start != 0, c->err);
+    c->map_fresh = false;
     if (rc == KS_OK) c->have_solution = true;   // r.flow_value: measured on device from the resident flow
     r.status = rc;
     if (out) *out = r;
@@ -527,15 +531,22 @@ int ks_get_flows(ks_ctx* c, ks_flow* out, size_t cap, size_t* count) {
 int ks_get_task_mapping(ks_ctx* c, uint64_t* task, uint64_t* pu, size_t cap, size_t* count) {
     if (!c || !count) return KS_E_INVALID;
     if (!c->have_solution) return c->fail(KS_E_INVALID, "no successful solve on this context");
-    size_t nt = 0;
-    int rc = c->eng.task_pu(nullptr, 0, &nt, c->n_tasks, c->err);
-    if (rc) return rc;
-    uint64_t* dev = nullptr;
-    rc = c->eng.scratch(&dev, nt, c->err);
-    if (rc == KS_OK) rc = c->eng.task_pu(dev, nt, &nt, c->n_tasks, c->err);
-    std::vector<uint64_t> dense(nt);
-    if (rc == KS_OK) rc = c->eng.download(dense.data(), dev, nt * sizeof(uint64_t), c->err);
-    if (rc) return rc;
+    // one device decomposition per solve: the usual count-then-fill call pair
+    // reuses it
+    if (!c->map_fresh) {
+        size_t nt = 0;
+        int rc = c->eng.task_pu(nullptr, 0, &nt, c->n_tasks, c->err);
+        if (rc) return rc;
+        uint64_t* dev = nullptr;
+        rc = c->eng.scratch(&dev, nt, c->err);
+        if (rc == KS_OK) rc = c->eng.task_pu(dev, nt, &nt, c->n_tasks, c->err);
+        c->map_dense.resize(nt);
+        if (rc == KS_OK) rc = c->eng.download(c->map_dense.data(), dev, nt * sizeof(uint64_t), c->err);
+        if (rc) return rc;
+        c->map_fresh = true;
+    }
+    const std::vector<uint64_t>& dense = c->map_dense;
+    const size_t nt = dense.size();
     size_t k = 0, ti = 0;
     for (uint64_t id = 1; id < c->nodes.size() && ti < nt; ++id) {
         const NodeRec& r = c->nodes[id];
@@ -607,6 +618,7 @@ int ks_update_unsched_costs(ks_ctx* c, const uint64_t* ids, size_t k, int32_t mo
     int rc = c->eng.unsched_costs(ids, ids ? k : 0, mode, unsched_cost, continuation_cost, &ch, c->err);
     if (rc == KS_OK && ch) {
         c->have_solution = false;
+        c->map_fresh = false;
         c->flows_fresh = false;
     }
     if (changed) *changed = ch;
@@ -628,7 +640,7 @@ int ks_topology_stats(ks_ctx* c, uint64_t max_tasks_per_pu, const uint64_t* pu_i
     const int64_t sink = c->n_sinks == 1 ? (int64_t)c->sink_id - 1 : -1;
     int rc = c->eng.topology_stats(max_tasks_per_pu, pu_ids, pu_running, pu_ids ? k : 0, sink, slots_below,
                                    running_below, c->err);
-    if (!c->eng.solved()) c->have_solution = c->flows_fresh = false;   // a pending CSR rebuild ran
+    if (!c->eng.solved()) c->have_solution = c->flows_fresh = c->map_fresh = false;   // a pending CSR rebuild ran
     return rc;
 }
 

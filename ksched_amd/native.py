@@ -243,12 +243,17 @@ class Context:
         self._check(self._L.ks_get_flows(self._h, out.ctypes.data, cnt.value, C.byref(cnt)))
         return out
 
-    def task_mapping(self) -> dict[int, int]:
+    def task_mapping_arrays(self) -> tuple[np.ndarray, np.ndarray]:
+        """ks_get_task_mapping as the C-ABI returns it: parallel (task id, PU id) arrays."""
         cnt = C.c_size_t()
         self._check(self._L.ks_get_task_mapping(self._h, None, None, 0, C.byref(cnt)))
         t = np.zeros(cnt.value, np.uint64)
         p = np.zeros(cnt.value, np.uint64)
         self._check(self._L.ks_get_task_mapping(self._h, t.ctypes.data, p.ctypes.data, cnt.value, C.byref(cnt)))
+        return t[:cnt.value], p[:cnt.value]
+
+    def task_mapping(self) -> dict[int, int]:
+        t, p = self.task_mapping_arrays()
         return dict(zip(t.tolist(), p.tolist()))
 
     def store_stats(self) -> dict:

@@ -79,3 +79,17 @@ def test_pinned_task_has_only_its_running_arc():
     for t, p in list(mp.items())[:20]:
         out = [(int(d), int(lo), int(c)) for s, d, lo, c in zip(h.src, h.dst, h.low, h.cap) if s == t]
         assert out == [(p, 1, 1)]                        # graph_manager.go:690-735
+
+
+def test_step_takes_the_mapping_as_arrays():
+    """cell.step accepts ks_get_task_mapping's (task ids, PU ids) arrays (what the
+    config-4 bench times) and produces the same records as the dict form."""
+    import numpy as np
+    from ksched_amd import churn
+    a = churn.Cell(2_000, 200, 10, 20, 5)
+    b = churn.Cell(2_000, 200, 10, 20, 5)
+    tasks = a.task_ids(a.WAIT)[:500]
+    pus = a.PU0 + (np.arange(tasks.shape[0]) % 200)
+    da = a.step(dict(zip(tasks.tolist(), pus.tolist())), done=50, arrive=50)
+    db = b.step((tasks.astype(np.uint64), pus.astype(np.uint64)), done=50, arrive=50)
+    assert da.shape == db.shape and (da == db).all()
