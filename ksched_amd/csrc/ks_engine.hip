@@ -1472,6 +1472,9 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 #ifndef KS_HOP3
 #define KS_HOP3 0
 #endif
+#ifndef KS_HUB_LAZY
+#define KS_HUB_LAZY 0              // 1: hub chunks test the residual before the tail gathers (measured: no faster)
+#endif
 template <bool PR>
 __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
                            long long B, long long* hub_min, int& out);
@@ -1581,11 +1584,15 @@ __device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, lo
 
 // Relax in-arc (u→v) = reverse of CSR arc a = (v→u); residual ucap − rcap,
 // cost −cost(a). Loads are issued before the residual test (short chain).
-template <bool PR>
+// LAZY: test the residual before gathering the tail's record (hub chunks: a
+// hub's in-arcs are mostly saturated, and their gathers are most of a heavy
+// round's bytes; elsewhere the gathers issue with the arc for a shorter chain).
+template <bool PR, bool LAZY = false>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
                                          long long eps, long long B, long long* hub_min, int& out) {
     const Pos q = ld_pos(g.pos + a);
     const long long rin = q.ucap - q.rcap;
+    if (LAZY && rin <= 0) return;
     const int u = q.head;
     const long long ca = q.cost;
     const long long pu = g.p0[ni(u)];
@@ -1734,7 +1741,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR>(g, N, a, dv, pv, eps, B, hub_min, out);
+                        relax_in<PR, KS_HUB_LAZY != 0>(g, N, a, dv, pv, eps, B, hub_min, out);
                         scans++;
                     }
                 }
@@ -2402,6 +2409,9 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
         }
         return;
     }
+    // listed nodes: one wave each, 64 arcs per pass (eight nodes per wave with eight
+    // lanes each was measured slower: a wave then walked its wider nodes — machines —
+    // one after another, lengthening the round's chain)
     const int nw = ((int)gridDim.x - nhb) * WPB;
     for (int i = ((int)blockIdx.x - nhb) * WPB + (int)(threadIdx.x >> 6); i < cnt; i += nw) {
         const int v = g.fl[(size_t)lin * g.fl_cap + i];
