@@ -149,12 +149,16 @@ struct Ctl {
     int fs_cnt[3];         // frontier list lengths (rotating like the flag buffers)
     int fs_done;           // the search's frontier drained
     int fs_fail;           // list overflow or no deficit in range: the next cycle is a backward update
-    int fs_pending;        // the search has not converged: the next cycle continues it
+    int fs_pending;        // a search is running: the next init continues it (set by its first round)
     int fs_rounds;         // rounds of the running search that had a frontier
     int n_fdef;            // deficits at distance D listed for the trace
     int fs_moved;          // units the trace moved
     long long u_exc;       // excess units the last apply (backward) / init (forward) found
     int fs_maxcnt;         // the running search's widest frontier (nodes; hubs count 1024 each)
+    int n_exc_rep;         // excess nodes / units the last completed forward update's init found
+    long long u_exc_rep;
+    int fs_completed;      // forward updates completed (whole solve)
+    int fs_moved_cyc;      // units the traces of this cycle moved
 };
 
 struct HItem {
@@ -1946,13 +1950,7 @@ __global__ void k_pr_init(DG g, int seq0) {
 __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
     static_assert(sizeof(Ctl) % 4 == 0, "Ctl is copied as words");
     if (threadIdx.x == 0) {
-        if (fwd) {
-            const int pend = (g.ctl->fs_done || g.ctl->fs_fail) ? 0 : 1;
-            g.ctl->fs_pending = pend;
-            if (!pend) g.ctl->fs_cnt[0] = g.ctl->fs_cnt[1] = g.ctl->fs_cnt[2] = 0;
-        } else {
-            g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;
-        }
+        if (!fwd) g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;   // (forward: k_fs_end)
     }
     __syncthreads();
     const int* src = reinterpret_cast<const int*>(g.ctl);
@@ -1961,10 +1959,13 @@ __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
         __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
     // a forward init counts excess nodes into n_exc from every block: zero it here
-    // (a backward init zeroes it itself); a search still running keeps its count
-    if (threadIdx.x == 0 && !(fwd && g.ctl->fs_pending)) {
-        g.ctl->n_exc = 0;
-        g.ctl->u_exc = 0;
+    // (a backward init zeroes it itself; forward updates: k_fs_end)
+    if (threadIdx.x == 0) {
+        if (!fwd) {
+            g.ctl->n_exc = 0;
+            g.ctl->u_exc = 0;
+        }
+        g.ctl->fs_moved_cyc = 0;
     }
     __threadfence_system();
 }
@@ -2383,6 +2384,7 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
         for (int h = 0; h < g.nheavy; ++h) hub_any += F.hub[h];
         if (cnt == 0 && !hub_any) g.ctl->fs_done = 1;   // empty frontier: converged
         else {
+            g.ctl->fs_pending = 1;   // the next init (this cycle's or the next's) continues it
             g.ctl->fs_rounds += 1;
             atomicAdd(g.ctr + C_BFROUND, 1ULL);
             const int width = cnt + 1024 * hub_any;
@@ -2436,6 +2438,7 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
 // list the deficits found at distance D for the trace.
 __global__ void k_fs_apply(DG g) {
     if (!g.ctl->fs_done || g.ctl->fs_fail) return;
+    if (atom_load_i(&g.ctl->n_exc) == 0) return;   // no excess left: nothing to search from
     const long long D = atom_load(&g.ctl->fs_D);
     if (D >= FS_DMAX) {   // no deficit in range: a backward update decides (infeasible or not)
         if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->fs_fail = 1;
@@ -2548,10 +2551,25 @@ __global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
         if (all) {
             atom_add(&g.excess[t], amt);
             atomicAdd(&g.ctl->fs_moved, 1);
+            atomicAdd(&g.ctl->fs_moved_cyc, 1);
         } else {
             atom_add(&g.excess[src], amt);   // the unit stays for the next update
         }
     }
+}
+
+// End of a forward update: a finished (or failed) search releases the init and
+// reports its excess counts; one still running keeps them (its init is skipped).
+__global__ void k_fs_end(DG g) {
+    if (threadIdx.x || blockIdx.x) return;
+    if (!g.ctl->fs_done && !g.ctl->fs_fail) return;
+    g.ctl->fs_pending = 0;
+    g.ctl->fs_cnt[0] = g.ctl->fs_cnt[1] = g.ctl->fs_cnt[2] = 0;
+    g.ctl->n_exc_rep = atom_load_i(&g.ctl->n_exc);
+    g.ctl->u_exc_rep = atom_load(&g.ctl->u_exc);
+    g.ctl->n_exc = 0;
+    g.ctl->u_exc = 0;
+    if (g.ctl->fs_done && !g.ctl->fs_fail) g.ctl->fs_completed += 1;
 }
 
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
@@ -4197,7 +4215,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
         bool fwd_off = false; // a forward search ran past its round budget: backward updates for the rest of the phase
-        int fs_used = 0;      // rounds enqueued for the running forward search
         int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
         // tail progress per mode (excess units routed per ms of device time): once the
         // last phase's forward updates route fewer than a quarter of the units per ms
@@ -4227,21 +4244,28 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int rc = KS_OK;
         // Forward cycle: [init (or continue the pending search)][kf rounds][apply]
         // [trace][end]; no sweeps (the trace routes the units).
-        auto enqueue_fwd = [&](int par) -> hipError_t {
-            hipLaunchKernelGGL(k_fs_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
-            for (int r = 0; r < kf; ++r) {
-                hipLaunchKernelGGL(k_fs_round, dim3(fsgrid), dim3(BLK), 0, st, g, bseq);
-                ++bseq;
-                ++bf_launches;
+        // nupd updates back to back in one cycle (one host round trip): an update
+        // whose search has not converged when the next one starts is continued by it.
+        auto enqueue_fwd = [&](int par, int nupd) -> hipError_t {
+            hipError_t e = hipSuccess;
+            for (int u = 0; u < nupd; ++u) {
+                hipLaunchKernelGGL(k_fs_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+                for (int r = 0; r < kf; ++r) {
+                    hipLaunchKernelGGL(k_fs_round, dim3(fsgrid), dim3(BLK), 0, st, g, bseq);
+                    ++bseq;
+                    ++bf_launches;
+                }
+                if (u == 0 && (e = hipEventRecord(s.cev[par][0], st)) != hipSuccess) return e;
+                hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
+                hipLaunchKernelGGL(k_fs_trace, dim3(FDEF_CAP), dim3(WAVE), 0, st, g);
+                hipLaunchKernelGGL(k_fs_end, dim3(1), dim3(WAVE), 0, st, g);
             }
-            hipError_t e = hipEventRecord(s.cev[par][0], st);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
             if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_fs_trace, dim3(FDEF_CAP), dim3(WAVE), 0, st, g);
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
             return hipEventRecord(s.cdone[par], st);
         };
+        int nupd = 1;         // forward updates per cycle (2 once a search finished within its rounds)
+        int completed0 = 0;   // fs_completed at the phase's start of forward cycles
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
@@ -4277,39 +4301,39 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (use_fwd) {   // a phase never continues another phase's forward search
             KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
+            KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_completed, 0, sizeof(int), st));
         }
         KS_CHECK(hipEventRecord(s.cstart, st));
         hipEvent_t prev_end = s.cstart;
         int cur = 0;
         for (;;) {
             if (fwd) {
-                KS_CHECK(enqueue_fwd(cur));
+                KS_CHECK(enqueue_fwd(cur, nupd));
                 KS_CHECK(hipEventSynchronize(s.cdone[cur]));
                 const Ctl* hc = s.h_cyc[cur];
-                const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][1], s.cdone[cur]);
+                const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][0], s.cdone[cur]);
                 ms_bf_k += t_bf;
                 ms_sw_k += t_sw;
                 prev_end = s.cdone[cur];
                 cur ^= 1;
-                fs_used += kf;
                 acc_ms += t_bf + t_sw;
+                const bool completed = hc->fs_done || hc->fs_fail;
                 if (cycle_log)
-                    std::fprintf(stderr, "fwd cycle phase %d eps %lld rounds %d bf_ms %.3f tr_ms %.3f units %lld n_exc %d done %d fail %d D %lld deficits %d moved %d width %d\n",
-                                 phases, eps_ph, hc->fs_rounds, t_bf, t_sw, hc->u_exc, hc->n_exc, hc->fs_done, hc->fs_fail,
-                                 hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef, hc->fs_moved, hc->fs_maxcnt);
-                if (hc->n_exc == 0) break;   // no excess left: the phase is done
-                const bool completed = hc->fs_done || hc->fs_fail || fs_used >= fwd_budget;
-                if (KS_FWD_EXIT && hc->fs_done && !hc->fs_fail && may_end_early && hc->n_exc <= phase_exit &&
-                    (long long)hc->n_exc * phase_frac <= phase_peak) {
-                    ++early_exits;   // a coarse phase ends as after a global update (the same rule)
-                    break;
-                }
+                    std::fprintf(stderr, "fwd cycle phase %d eps %lld updates %d rounds %d bf_ms %.3f tr_ms %.3f units %lld n_exc %d done %d fail %d D %lld deficits %d moved %d width %d\n",
+                                 phases, eps_ph, nupd, hc->fs_rounds, t_bf, t_sw, hc->u_exc_rep, hc->n_exc_rep,
+                                 hc->fs_done, hc->fs_fail, hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef,
+                                 hc->fs_moved_cyc, hc->fs_maxcnt);
+                if (completed && hc->n_exc_rep == 0) break;   // no excess left: the phase is done
                 if (completed) {
-                    account(1, true, acc_ms, hc->u_exc);
+                    account(1, true, acc_ms, hc->u_exc_rep);
                     acc_ms = 0;
                 }
+                const int done_now = hc->fs_completed - completed0;
+                completed0 = hc->fs_completed;
+                gus += done_now;
+                fwd_updates += done_now;
                 bool wide = hc->fs_fail == 2;
-                if (!hc->fs_fail && !hc->fs_done && fs_used >= fwd_budget && !KS_FWD_FIXED) {
+                if (!completed && hc->fs_rounds >= fwd_budget && !KS_FWD_FIXED) {
                     // longer than two global updates: drop it like a wide one
                     KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
                     KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
@@ -4322,23 +4346,22 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     fwd = 0;
                     fwd_block = 1;
                     fwd_off = fwd_off || wide;
-                    fs_used = 0;
+                    nupd = 1;
                     continue;
                 }
-                if (!hc->fs_done) {          // the search continues next cycle
+                if (!completed) {            // the search continues next cycle
                     kf = std::min(256, 2 * kf);
+                    nupd = 1;
                     continue;
                 }
-                fs_used = 0;
-                ++gus;
-                ++fwd_updates;
                 kf = std::max(8, std::min(256, hc->fs_rounds + 4));
+                nupd = 2;
                 if (!KS_FWD_FIXED && fwd_worse()) {
                     fwd = 0;
                     fwd_off = true;
                     continue;
                 }
-                if (hc->fs_moved == 0) {
+                if (hc->fs_moved_cyc == 0) {
                     fwd = 0;
                     fwd_block = 1;
                 }
