@@ -109,6 +109,9 @@ constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess nod
 constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
+#ifndef KS_FWD_UPD
+#define KS_FWD_UPD 4               // forward updates per cycle once a search finished within its rounds (2: ~1 ms slower on config 4)
+#endif
 #ifndef KS_FWD_LAST
 #define KS_FWD_LAST 0              // 1: forward updates in the last phase too (guarded by the rate rule)
 #endif
@@ -4264,7 +4267,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
             return hipEventRecord(s.cdone[par], st);
         };
-        int nupd = 1;         // forward updates per cycle (2 once a search finished within its rounds)
+        int nupd = 1;         // forward updates per cycle (KS_FWD_UPD once a search finished within its rounds)
         int completed0 = 0;   // fs_completed at the phase's start of forward cycles
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
@@ -4355,7 +4358,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     continue;
                 }
                 kf = std::max(8, std::min(256, hc->fs_rounds + 4));
-                nupd = 2;
+                nupd = KS_FWD_UPD;
                 if (!KS_FWD_FIXED && fwd_worse()) {
                     fwd = 0;
                     fwd_off = true;
