@@ -109,6 +109,9 @@ constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess nod
 constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
+#ifndef KS_FWD_WIDE_OFF
+#define KS_FWD_WIDE_OFF 1          // a wide search ends a coarse phase's forward updates (0: one global update, then again)
+#endif
 #ifndef KS_FWD_UPD
 #define KS_FWD_UPD 4               // forward updates per cycle once a search finished within its rounds (2: ~1 ms slower on config 4)
 #endif
@@ -4348,7 +4351,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     // a global one): global updates for the rest of the phase
                     fwd = 0;
                     fwd_block = 1;
-                    fwd_off = fwd_off || wide;
+                    fwd_off = fwd_off || (wide && (!may_end_early || KS_FWD_WIDE_OFF));
                     nupd = 1;
                     continue;
                 }
