@@ -110,7 +110,7 @@ constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
 #ifndef KS_FWD_WIDE_OFF
-#define KS_FWD_WIDE_OFF 1          // a wide search ends a coarse phase's forward updates (0: one global update, then again)
+#define KS_FWD_WIDE_OFF 0          // 1: a wide or overlong search ends a coarse phase's forward updates (0: one global update, then forward again; config 4 -2..4 ms, config 3 never runs them)
 #endif
 #ifndef KS_FWD_UPD
 #define KS_FWD_UPD 4               // forward updates per cycle once a search finished within its rounds (2: ~1 ms slower on config 4)
