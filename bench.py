@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 B_UNIT = 24             # bytes per residual-arc scan / node visit / push / relaxation
 B_RELAX = 44            # Bellman-Ford in-arc relaxation as the kernel reads it: ucap, rcap, cost (8 each),
                         # head (4), gathered price and distance of the tail (8 each) — second field
-PMC_FILE = os.path.join(ROOT, "profiles", "r03l_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03m_pmc_traffic.json")
 
 
 def roofline_of(results):
