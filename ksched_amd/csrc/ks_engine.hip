@@ -43,7 +43,12 @@
 //   tail       once an update leaves ≤ 64 nodes with excess, each sends its
 //              units down the update's distances (k_augment walks; k_aug_hub
 //              hands a hub's excess on in parallel) instead of one hop per
-//              sweep over dozens of cycles.
+//              sweep over dozens of cycles; the update itself is bounded at the
+//              excess nodes' largest distance. In a coarse phase the tail runs
+//              FORWARD updates instead (k_fs_*): a search from the excess nodes
+//              to the nearest deficit, the successive-shortest-path dual step,
+//              and one unit per deficit pushed back along the search's parent
+//              arcs — no global recompute.
 //   verify     on-device: conservation, capacity, and 1-optimality of the final
 //              prices in scaled units (costs × (n+1), so 1-optimal ⇒ optimal);
 //              the total cost is reduced in int64.
@@ -2301,8 +2306,9 @@ __device__ __forceinline__ void fs_append(const DG& g, int l, bool on, int v) {
 }
 
 // Init: every excess node is a source (d_f 0, no parent), everything else
-// unreached; the sources are the first round's frontier. A search that did not
-// converge last cycle (fs_pending) is continued instead.
+// unreached; the sources are the first round's frontier. A search still running
+// (fs_pending: set by its first round, cleared by k_fs_end once it finished —
+// in this cycle's earlier update or the last cycle) is continued instead.
 __global__ void k_fs_init(DG g, int seq0) {
     if (g.ctl->fs_pending) return;
     clear_fronts(g, g.bf);
