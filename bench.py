@@ -40,28 +40,64 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 B_UNIT = 24             # bytes per residual-arc scan / node visit / push / relaxation
 B_RELAX = 44            # Bellman-Ford in-arc relaxation as the kernel reads it: ucap, rcap, cost (8 each),
                         # head (4), gathered price and distance of the tail (8 each) — second field
-PMC_FILE = os.path.join(ROOT, "profiles", "r03m_pmc_traffic.json")
+# PMC traffic per workload: (FETCH_SIZE + WRITE_SIZE) per launch of each kernel,
+# from rocprofv3 --pmc passes of the same workload (tools/gpu_pmc.sh); the newest
+# file for the workload wins
+PMC_DIR = os.path.join(ROOT, "profiles")
 
 
-def roofline_of(results):
+def pmc_file(workload: str):
+    import glob
+    cands = sorted(glob.glob(os.path.join(PMC_DIR, f"r*_pmc_{workload}.json")))
+    if cands:
+        return cands[-1]
+    legacy = os.path.join(PMC_DIR, "r03m_pmc_traffic.json")   # round 3: config 3 only
+    return legacy if workload == "config3" and os.path.exists(legacy) else None
+
+
+# kinds of device work a solve reports (ks_result ABI 3): the kernel each one
+# times, its launch count and time fields, its algorithmic units
+KINDS = {
+    "k_sweep": ("sweep_launches", "ms_sweep_kernels", ("arc_scans", "node_visits", "pushes")),
+    "k_bf_round": ("gu_launches", "ms_gu_kernels", ("gu_arc_scans",)),
+    "k_fs_round": ("fs_launches", "ms_fs_kernels", ()),
+    "k_cell": (None, "ms_cell_kernel", ("arc_scans", "node_visits", "pushes", "gu_arc_scans")),
+}
+
+
+def pct(xs, q):
+    return round(float(np.percentile(np.asarray(xs, float), q)), 3) if len(xs) else None
+
+
+def latency_stats(step_ms):
+    """p50 / p95 / max of the timed steps (a scheduler's round budget is set by the max)."""
+    if not step_ms:
+        return None
+    return {"p50_ms": pct(step_ms, 50), "p95_ms": pct(step_ms, 95), "max_ms": round(max(step_ms), 3),
+            "min_ms": round(min(step_ms), 3), "max_over_median": round(max(step_ms) / float(np.median(step_ms)), 3)}
+
+
+def roofline_of(results, workload: str):
     """HBM roofline of the dominant kernel (by event-timed device time) over the
     timed steps: algorithmic bytes = SURVEY §8(d)'s 24 B per unit × the device
     counters' units, divided by the HIP-event-timed duration of that kernel's
-    launches (measured on the engine's stream). For k_bf_round the 44 B the
-    relaxation actually reads is reported beside it. ``traffic`` (PMC bytes per
-    launch) cannot be collected inside this run (rocprofv3 --pmc is its own
-    pass): it is read from the dated profile named in ``traffic_source``."""
+    launches (each kind's span brackets exactly its own kernels, ks_result ABI 3).
+    For k_bf_round the 44 B the relaxation actually reads is reported beside it;
+    the forward search (k_fs_round) has no unit counter and is reported by time.
+    The cell solver (k_cell, one launch per solve) does all four kinds of work
+    in one kernel: its units are all of them. ``traffic`` (PMC bytes per launch)
+    cannot be collected inside this run (rocprofv3 --pmc is its own pass): it is
+    read from the newest profile of the SAME workload, named in traffic_source."""
     n_res = max(1, len(results))
-    sw_ms = sum(r.raw["ms_sweep_kernels"] for r in results)
-    bf_ms = sum(r.raw["ms_gu_kernels"] for r in results)
-    sw_n = sum(r.raw["sweep_launches"] for r in results)
-    bf_n = sum(r.raw["gu_launches"] for r in results)
-    sw_units = sum(r.raw["arc_scans"] + r.raw["node_visits"] + r.raw["pushes"] for r in results)
-    bf_units = sum(r.raw["gu_arc_scans"] for r in results)
-    if sw_ms >= bf_ms:
-        kernel, ms, n, units = "k_sweep", sw_ms, sw_n, sw_units
-    else:
-        kernel, ms, n, units = "k_bf_round", bf_ms, bf_n, bf_units
+    kinds = {}
+    for kname, (nkey, mskey, ukeys) in KINDS.items():
+        rs = [r for r in results if (r.raw["solver"] == 1) == (kname == "k_cell")]
+        ms = sum(r.raw[mskey] for r in rs)
+        n = sum(r.raw[nkey] for r in rs) if nkey else sum(1 for r in rs if r.raw[mskey] > 0)
+        units = sum(sum(r.raw[u] for u in ukeys) for r in rs)
+        kinds[kname] = {"ms": ms, "launches": n, "units": units}
+    kernel = max(kinds, key=lambda k: kinds[k]["ms"])
+    ms, n, units = kinds[kernel]["ms"], kinds[kernel]["launches"], kinds[kernel]["units"]
     b = B_UNIT * units
     achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     line = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
@@ -69,10 +105,9 @@ def roofline_of(results):
             "bytes_per_unit": B_UNIT, "units_per_launch": round(units / max(1, n), 1),
             "bytes_per_launch": round(b / max(1, n), 1), "avg_launch_us": round(1e3 * ms / max(1, n), 3),
             "launches": n, "kernel_ms_per_step": round(ms / n_res, 3),
-            "other_kernel": {"k_sweep": {"ms_per_step": round(sw_ms / n_res, 3), "launches": sw_n,
-                                         "units": sw_units},
-                             "k_bf_round": {"ms_per_step": round(bf_ms / n_res, 3), "launches": bf_n,
-                                            "units": bf_units}}}
+            "kinds": {k: {"ms_per_step": round(v["ms"] / n_res, 3), "launches": v["launches"], "units": v["units"],
+                          "avg_launch_us": round(1e3 * v["ms"] / max(1, v["launches"]), 3)}
+                      for k, v in kinds.items() if v["ms"] > 0}}
     if kernel == "k_bf_round":
         a44 = B_RELAX * units / (ms / 1e3) / 1e9 if ms > 0 else 0.0
         line["achieved_44B"] = round(a44, 3)
@@ -80,6 +115,8 @@ def roofline_of(results):
     # SURVEY §8(d) solve-level figure: B_work = 24 B × (arc scans + node visits + pushes)
     # over the whole solve time (and with the Bellman-Ford relaxations added), and the
     # single-pass floor B_pass = 2m·16 + n·24 for scale
+    sw_units = sum(r.raw["arc_scans"] + r.raw["node_visits"] + r.raw["pushes"] for r in results)
+    bf_units = sum(r.raw["gu_arc_scans"] for r in results)
     t_solve = sum(r.raw["ms"]["total"] for r in results) / 1e3
     if t_solve > 0:
         nn, mm = results[-1].raw["n_nodes"], results[-1].raw["n_arcs"]
@@ -94,11 +131,12 @@ def roofline_of(results):
             "b_pass_bytes": bp, "b_pass_us_at_peak": round(bp / (HBM_PEAK_GBS * 1e9) * 1e6, 2),
             "note": "SURVEY 8(d): B_work / t_solve over all timed solves; b_pass = one read of the "
                     "residual graph, the floor any iterative solve sits above"}
-    if os.path.exists(PMC_FILE):
-        pmc = json.load(open(PMC_FILE))
+    pf = pmc_file(workload)
+    if pf:
+        pmc = json.load(open(pf))
         k = pmc.get("kernels", {}).get(kernel, {})
         line["traffic"] = k.get("raw_bytes_per_launch")
-        line["traffic_source"] = {"file": os.path.relpath(PMC_FILE, ROOT), "date": pmc.get("date"),
+        line["traffic_source"] = {"file": os.path.relpath(pf, ROOT), "date": pmc.get("date"),
                                   "workload": pmc.get("workload"),
                                   "calibrated_bytes_per_launch": k.get("calibrated_bytes_per_launch"),
                                   "atomics_per_launch": k.get("tcc_atomic_per_launch"),
@@ -317,8 +355,8 @@ def run_full(args, D):
               "tasks": T, "machines": M, "racks": R, "jobs": J, "seed": seed, "n": g.n, "m": g.m,
               "parallelism": f"independent graphs x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
-                     roofline=roofline_of(results), cpu_baseline=cpu, parity=parity, gather=gather,
-                     solve=dict(results[-1].raw))
+                     roofline=roofline_of(results, args.config), cpu_baseline=cpu, parity=parity, gather=gather,
+                     latency=latency_stats(step_ms), solve=dict(results[-1].raw))
     ctx.close()
     return line
 
@@ -353,7 +391,7 @@ def run_incremental(args, D):
         inc_first_ms = 1e3 * (time.perf_counter() - t0)
         if (c, f) != (r0.cost, r0.flow):
             problems.append(f"initial solve: GPU {r0.cost}/{r0.flow} vs CPU {c}/{f}")
-        cold_ms, inc_ms = [], []
+        cold_ms, inc_ms, cs_ms = [], [], []
     for i in range(args.warmup + args.steps):
         d = cell.step(mp, done=done, arrive=arrive)
         fresh = list(cell.last_arrived_ids)
@@ -388,10 +426,15 @@ def run_incremental(args, D):
             t0 = time.perf_counter()
             st2, c2, f2, _, _ = ko.reference_path(g)
             cold_ms.append(1e3 * (time.perf_counter() - t0))
-            rec["cpu"] = {"incremental_ms": round(inc_ms[-1], 1), "cold_ms": round(cold_ms[-1], 1), "cost": c,
+            t0 = time.perf_counter()
+            st3, c3, f3, _ = ko.cost_scaling(g)
+            cs_ms.append(1e3 * (time.perf_counter() - t0))
+            rec["cpu"] = {"incremental_ms": round(inc_ms[-1], 1), "cold_ms": round(cold_ms[-1], 1),
+                          "cost_scaling_ms": round(cs_ms[-1], 1), "cost": c,
                           "incremental_phases_ms": {k: round(v, 1) for k, v in inc.last["ms"].items()}}
-            if not ((r.cost, r.flow) == (c, f) == (c2, f2) and st == st2 == 0):
-                problems.append(f"round {i + 1}: GPU {r.cost}/{r.flow} vs CPU incremental {c}/{f}, cold {c2}/{f2}")
+            if not ((r.cost, r.flow) == (c, f) == (c2, f2) == (c3, f3) and st == st2 == st3 == 0):
+                problems.append(f"round {i + 1}: GPU {r.cost}/{r.flow} vs CPU incremental {c}/{f}, cold {c2}/{f2}, "
+                                f"cost scaling {c3}/{f3}")
         if i >= args.warmup:
             t_total += dt
             results.append(r)
@@ -408,17 +451,28 @@ def run_incremental(args, D):
     if cpu_on:
         ti = [x for x, rr in zip(inc_ms, rounds) if rr["timed"]]
         tc = [x for x, rr in zip(cold_ms, rounds) if rr["timed"]]
-        med_i, med_c = float(np.median(ti)), float(np.median(tc))
-        cpu = {"value": round(m_avg / (med_i / 1e3), 1), "unit": "arcs/s", "cores": 1, "kind": "port",
-               "sample": f"the same {len(ti)} timed rounds through the restatement of the reference's incremental mode "
-                         f"(ExportIncremental text -> parse -> incremental SSP from the previous round's flow and "
-                         f"potentials -> f lines -> BFS mapping; Flowlessly daemon, solver.go:30-34,86-89), median "
-                         f"per round, 1 thread",
-               "ms": round(med_i, 1), "times_ms": [round(x, 1) for x in ti], "first_full_solve_ms": round(inc_first_ms, 1),
-               "cold_reference_path": {"value": round(m_avg / (med_c / 1e3), 1), "unit": "arcs/s", "ms": round(med_c, 1),
-                                       "times_ms": [round(x, 1) for x in tc], "cores": 1,
-                                       "sample": "each timed round's full graph through the cold reference path "
-                                                 "(export -> SSP -> f lines -> BFS), median"}}
+        ts3 = [x for x, rr in zip(cs_ms, rounds) if rr["timed"]]
+        med_i, med_c, med_s = float(np.median(ti)), float(np.median(tc)), float(np.median(ts3))
+        inc_leg = {"value": round(m_avg / (med_i / 1e3), 1), "unit": "arcs/s", "ms": round(med_i, 1),
+                   "times_ms": [round(x, 1) for x in ti], "first_full_solve_ms": round(inc_first_ms, 1), "cores": 1,
+                   "sample": "the restatement of the reference's incremental mode (ExportIncremental text -> parse "
+                             "-> incremental SSP from the previous round's flow and potentials -> f lines -> BFS "
+                             "mapping; Flowlessly daemon, solver.go:30-34,86-89), median per round"}
+        cold_leg = {"value": round(m_avg / (med_c / 1e3), 1), "unit": "arcs/s", "ms": round(med_c, 1),
+                    "times_ms": [round(x, 1) for x in tc], "cores": 1,
+                    "sample": "each timed round's full graph through the cold reference path (export -> SSP -> "
+                              "f lines -> BFS), median"}
+        # headline: the FASTER of the two reference-path restatements
+        head, other, oname = (inc_leg, cold_leg, "cold_reference_path") if med_i <= med_c else \
+            (cold_leg, inc_leg, "incremental_reference_path")
+        cpu = {"value": head["value"], "unit": "arcs/s", "cores": 1, "kind": "port",
+               "sample": f"the same {len(ti)} timed rounds, the faster of two restatements of the reference CPU "
+                         f"path: " + head["sample"] + ", 1 thread",
+               "ms": head["ms"], "times_ms": head["times_ms"], oname: other,
+               "strong_cpu_cost_scaling": {"value": round(m_avg / (med_s / 1e3), 1), "unit": "arcs/s",
+                                           "ms": round(med_s, 1), "times_ms": [round(x, 1) for x in ts3],
+                                           "cores": 1, "sample": "each timed round's full graph through the "
+                                                                 "in-repo single-threaded cost-scaling oracle"}}
     config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
                           f"{arrive} arrivals per round, pins/ageing/capacity deltas; step = apply deltas + "
                           f"{'warm-started' if args.warm else 'from-scratch'} re-solve + mapping; {args.steps} timed "
@@ -427,7 +481,8 @@ def run_incremental(args, D):
               "round_ms": {"median": round(float(np.median([x["ms"] for x in timed])), 3),
                            "max": round(max(x["ms"] for x in timed), 3)},
               "parallelism": f"independent cells x{D.world}"}
-    line = base_line(args, D, value, ms_per_step, config, rounds=rounds, roofline=roofline_of(results),
+    line = base_line(args, D, value, ms_per_step, config, rounds=rounds, roofline=roofline_of(results, "config4"),
+                     latency=latency_stats([x["ms"] for x in timed]),
                      cpu_baseline=cpu, parity=parity)
     ctx.close()
     return line
@@ -534,14 +589,25 @@ def run_batch(args, D):
             with ThreadPoolExecutor(cores) as ex:
                 return list(ex.map(ko.reference_path, every))
         med, ts, outs, _ = timed_cpu(all_graphs_cpu, reps=args.cpu_reps, pin=False)
+
+        def all_graphs_cs():
+            with ThreadPoolExecutor(cores) as ex:
+                return list(ex.map(ko.cost_scaling, every))
+        med_s, ts_s, outs_s, _ = timed_cpu(all_graphs_cs, reps=args.cpu_reps, pin=False)
         m2 = gen.quincy_sizes(T, M, R, J)[1]
         cpu = {"value": round(num * m2 / med, 1), "unit": "arcs/s", "cores": cores, "kind": "port",
                "sample": f"all {num} graphs through the restatement of the reference CPU path (export -> SSP -> "
                          f"f lines -> BFS), one graph per thread on {cores} threads (the host cores this process "
                          f"may use), median of {len(ts)} after 1 warm-up",
-               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts)}
+               "ms": round(1e3 * med, 1), "times_ms": [round(1e3 * x, 1) for x in ts], "median_of": len(ts),
+               "strong_cpu_cost_scaling": {"value": round(num * m2 / med_s, 1), "unit": "arcs/s", "cores": cores,
+                                           "ms": round(1e3 * med_s, 1), "times_ms": [round(1e3 * x, 1) for x in ts_s],
+                                           "median_of": len(ts_s),
+                                           "sample": f"all {num} graphs through the in-repo cost-scaling oracle, one "
+                                                     f"graph per thread on {cores} threads"}}
         parity.update({"checked_graphs": num,
-                       "match": bool(per_graph is not None and all(o[1] == int(c) for o, c in zip(outs, per_graph)))})
+                       "match": bool(per_graph is not None and all(o[1] == int(c) == s[1] for o, c, s in
+                                                                   zip(outs, per_graph, outs_s)))})
         if not parity["match"]:
             parity["problems"] = ["a graph's GPU cost differs from the CPU reference path"]
     mode = {"abi": "C-ABI batch (union per device, RCCL gather inside libksmcmf)",
@@ -552,8 +618,8 @@ def run_batch(args, D):
               "graphs": num, "tasks": T, "machines": M, "graphs_per_gpu": len(mine), "mode": args.batch_mode,
               "parallelism": f"graph sharding x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
-                     roofline=roofline_of(results), cpu_baseline=cpu, gather=gather, parity=parity,
-                     cell_latency=extra_cells, solve=dict(results[-1].raw))
+                     roofline=roofline_of(results, "config5"), cpu_baseline=cpu, gather=gather, parity=parity,
+                     latency=latency_stats(step_ms), cell_latency=extra_cells, solve=dict(results[-1].raw))
     if args.batch_mode == "abi":
         bt.close()
     else:

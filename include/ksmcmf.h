@@ -64,7 +64,11 @@
 extern "C" {
 #endif
 
-#define KSMCMF_ABI_VERSION 2   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls */
+#define KSMCMF_ABI_VERSION 3   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls;
+                                  3: ks_opts.cell_nodes, ks_result per-kind timing and cell-solver
+                                  fields. ks_opts (96 B) and ks_result (320 B) CHANGED SIZE in
+                                  ABI 2 and ks_result again in ABI 3: a caller must check
+                                  ks_abi_version() == KSMCMF_ABI_VERSION before ks_create. */
 
 /* status codes (0 = OK) */
 #define KS_OK            0
@@ -114,7 +118,10 @@ typedef struct ks_opts {
     int32_t  fault_inject;     /* TESTS ONLY [0]: bit 0 — the last phase's walks use the
                                   coarse slack at ε = 1 (may end non-1-optimal); bit 1 —
                                   the final prices are perturbed before verification.
-                                  Both must be repaired by the certificate recovery.    */
+                                  Both must be repaired by the certificate recovery.
+                                  Bit 2 (ks_batch_create*): global rank 0 fails to pack
+                                  its rows in ks_batch_gather (every rank must still
+                                  reach the collective and return the error).          */
     int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
                                   cycle [1]; later passes retry units left short        */
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —
@@ -123,13 +130,19 @@ typedef struct ks_opts {
     int32_t  bf_bound;         /* a global update with ≤ 64 excess nodes drops Bellman-Ford
                                   offers at or above the largest tentative distance of
                                   those nodes and caps prices there [on]; < 0 off       */
-    int32_t  fwd_nodes;        /* once ≤ fwd_nodes nodes hold excess, a cycle searches
-                                  from them to the nearest deficit and pushes along the
-                                  search's shortest paths instead of a global update;
-                                  a search that takes more than half the rounds of the
-                                  last global update, or a cycle more than half its time,
-                                  ends them for the phase [64]; < 0 off                 */
-    int32_t  reserved[4];
+    int32_t  fwd_nodes;        /* in a coarse phase (one a finer phase follows), once
+                                  ≤ fwd_nodes nodes hold excess, a cycle searches from them
+                                  to the nearest deficit and pushes along the search's
+                                  shortest paths instead of a global update [64]; a search
+                                  whose frontier grows past n/4 nodes, or that runs longer
+                                  than twice the last global update's rounds, costs ONE
+                                  global update and the next cycle searches forward again.
+                                  The last phase always uses global updates. < 0 off      */
+    int32_t  cell_nodes;       /* the cell solver (one workgroup per graph)
+                                  solves every graph — or every cell of a ks_batch union —
+                                  of at most cell_nodes node slots [0: as many as its LDS
+                                  holds, 13,2xx]; < 0: always the multi-kernel engine    */
+    int32_t  reserved[3];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */
@@ -194,7 +207,21 @@ typedef struct ks_result {
     int32_t  recoveries;       /* times the final optimality certificate failed and was
                                   repaired (price refinement, else one more ε = 1 phase
                                   from the current flow) before the solve returned      */
-    int32_t  _pad;
+    int32_t  solver;           /* 0: multi-kernel engine; 1: cell solver (ABI 3)         */
+    /* ABI 3. Per-kind device time: each span starts at an event recorded right before
+       its first kernel and ends at one right after its last (no host gap inside).
+       ms_gu_kernels / gu_launches: the backward Bellman-Ford rounds (global updates,
+       price refinement); ms_sweep_kernels / sweep_launches: the sweep bursts;
+       forward tail updates (k_fs_*) are their own kind:                               */
+    uint64_t fs_launches;      /* forward search rounds launched (k_fs_round)           */
+    double   ms_fs_kernels;    /* event-timed span of the forward-update batches (ms)   */
+    uint64_t fwd_updates;      /* forward tail updates completed                        */
+    int32_t  cells;            /* cells the cell solver ran (one workgroup each)        */
+    int32_t  _pad3;
+    double   ms_cell_kernel;   /* event-timed duration of the cell-solver launches (ms) */
+    uint64_t cell_ticks_max;   /* slowest cell's in-kernel solve time (100 MHz ticks)   */
+    uint64_t cell_ticks_sum;   /* Σ over cells of their in-kernel solve times            */
+    uint64_t reserved2[4];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

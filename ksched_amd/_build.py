@@ -10,9 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libksmcmf.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("ks_engine.hip", "ks_store.hip", "ks_sched.hip", "ks_batch.hip",
-                                           "ks_host.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("ks_engine.h", "ks_store.h", "ks_sched.h", "ks_ctx.h", "ks_pos.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("ks_engine.hip", "ks_cell.hip", "ks_store.hip", "ks_sched.hip",
+                                           "ks_batch.hip", "ks_host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("ks_engine.h", "ks_cell.h", "ks_store.h", "ks_sched.h", "ks_ctx.h",
+                                                  "ks_pos.h")] + [
     os.path.join(ROOT, "include", "ksmcmf.h")]
 
 

@@ -123,6 +123,7 @@ struct ks_batch {
     std::string err;
     long long* root_buf = nullptr;      // rank 0: world × slots × rowlen
     size_t root_cap = 0;
+    int fault_pack = 0;                 // TESTS ONLY (ks_opts.fault_inject bit 2): global rank + 1 whose packing fails
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -147,13 +148,20 @@ ks_batch* make_batch(int world, const ks_opts* opts, const std::vector<std::pair
     ks_batch* b = new (std::nothrow) ks_batch;
     if (!b) return nullptr;
     b->world = world;
+    b->fault_pack = (opts && (opts->fault_inject & 4)) ? 1 : 0;   // TESTS ONLY: global rank 0's packing fails
     for (auto [dev, rank] : dev_rank) {
         ks_batch::Local l;
         l.device = dev;
         l.grank = rank;
         l.ctx = ks_create(dev, opts);
-        if (!l.ctx) {
-            for (auto& x : b->loc) ks_destroy(x.ctx);
+        // the status word of the gather's all-reduce exists before any gather, so a
+        // rank can always enter that collective
+        if (!l.ctx || hipSetDevice(dev) != hipSuccess || hipMalloc(&l.stat, sizeof(long long)) != hipSuccess) {
+            if (l.ctx) ks_destroy(l.ctx);
+            for (auto& x : b->loc) {
+                if (x.stat) (void)hipFree(x.stat);
+                ks_destroy(x.ctx);
+            }
             delete b;
             return nullptr;
         }
@@ -300,6 +308,8 @@ int ks_batch_load(ks_batch* b, size_t ngraphs, const ks_node* const* nodes, cons
         }
         const int rc = ks_load_graph(l.ctx, un.data(), un.size(), ua.data(), ua.size());
         if (rc) return b->fail(rc, ks_last_error(l.ctx));
+        // the union's cells: the cell solver runs each in its own workgroup (ks_cell.h)
+        l.ctx->eng.set_cells(l.off.data(), l.graphs.size());
     }
     return KS_OK;
 }
@@ -324,25 +334,42 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
     const size_t block = kb_block(b->ngraphs, b->world, max_tasks);   // elements per rank
     bool has_root = false;
     // 1. every device packs its block: [status][rows: cost, flow value, cell-local PU per task].
-    //    A rank that fails here still takes part in the collective below (with its
-    //    status word set), so its peers never wait for a send that is not posted.
+    //    A rank that fails here — a logical error or ANY HIP failure — still takes part
+    //    in the collective below with its status word set, so its peers never wait for
+    //    a send that is not posted (no early return before the status all-reduce).
     std::vector<int> status(b->loc.size(), KS_OK);
     std::string first_err;
     for (size_t li = 0; li < b->loc.size(); ++li) {
         auto& l = b->loc[li];
-        KB_HIP(hipSetDevice(l.device));
-        if (l.grank == 0) has_root = true;
         ks_ctx* c = l.ctx;
+        if (l.grank == 0) has_root = true;
         const size_t k = l.graphs.size();
         hipStream_t st = c->eng.stream();
-        if (l.rows_cap < block) {
+        int rc = KS_OK;
+        // a HIP failure: this rank's status, then on to the collective
+#define KB_TRY(expr)                                                                          \
+    do {                                                                                      \
+        if (rc == KS_OK) {                                                                    \
+            const hipError_t _e = (expr);                                                     \
+            if (_e != hipSuccess) {                                                           \
+                rc = KS_E_DEVICE;                                                             \
+                c->err = std::string(#expr) + ": " + hipGetErrorString(_e);                   \
+            }                                                                                 \
+        }                                                                                     \
+    } while (0)
+        KB_TRY(hipSetDevice(l.device));
+        if (b->fault_pack == (int)l.grank + 1) {   // TESTS ONLY: this rank's packing fails
+            rc = KS_E_DEVICE;
+            c->err = "injected pack failure";
+        }
+        if (rc == KS_OK && l.rows_cap < block) {
             if (l.rows) (void)hipFree(l.rows);
             l.rows = nullptr;
-            KB_HIP(hipMalloc(&l.rows, block * sizeof(long long)));
-            l.rows_cap = block;
+            l.rows_cap = 0;
+            KB_TRY(hipMalloc(&l.rows, block * sizeof(long long)));
+            if (rc == KS_OK) l.rows_cap = block;
         }
-        KB_HIP(hipMemsetAsync(l.rows, 0, block * sizeof(long long), st));
-        int rc = KS_OK;
+        KB_TRY(hipMemsetAsync(l.rows, 0, block * sizeof(long long), st));
         for (size_t i = 0; i < k && rc == KS_OK; ++i)
             if ((size_t)(l.toff[i + 1] - l.toff[i]) > max_tasks) {
                 rc = KS_E_INVALID;
@@ -352,8 +379,9 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
         if (rc == KS_OK && l.scratch_cap < need) {
             if (l.scratch) (void)hipFree(l.scratch);
             l.scratch = nullptr;
-            KB_HIP(hipMalloc(&l.scratch, std::max<size_t>(need, 1) * sizeof(long long)));
-            l.scratch_cap = need;
+            l.scratch_cap = 0;
+            KB_TRY(hipMalloc(&l.scratch, std::max<size_t>(need, 1) * sizeof(long long)));
+            if (rc == KS_OK) l.scratch_cap = need;
         }
         if (rc == KS_OK && k) {
             long long* dcost = l.scratch + l.toff.back();
@@ -362,59 +390,70 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
             rc = c->eng.cell_sums(l.off.data(), k, (int64_t*)dcost, (int64_t*)dflow, c->err);
             size_t cnt = 0;
             if (rc == KS_OK) rc = ks_get_task_pu_device(c, (uint64_t*)l.scratch, (size_t)l.toff.back(), &cnt);
-            if (rc == KS_OK) {
-                long long* rows = l.rows + kb_row_in_block(0, max_tasks);
-                KB_HIP(hipMemcpy2DAsync(rows, rowlen * sizeof(long long), dcost, sizeof(long long), sizeof(long long),
-                                        k, hipMemcpyDeviceToDevice, st));
-                KB_HIP(hipMemcpy2DAsync(rows + 1, rowlen * sizeof(long long), dflow, sizeof(long long),
-                                        sizeof(long long), k, hipMemcpyDeviceToDevice, st));
-                for (size_t i = 0; i < k; ++i) {
-                    const size_t t = (size_t)(l.toff[i + 1] - l.toff[i]);
-                    if (t)
-                        KB_HIP(hipMemcpyAsync(l.rows + kb_row_in_block(i, max_tasks) + 2, l.scratch + l.toff[i],
-                                              t * sizeof(long long), hipMemcpyDeviceToDevice, st));
-                }
-                KB_HIP(hipMemcpyAsync(doff, l.off.data(), k * sizeof(long long), hipMemcpyHostToDevice, st));
+            long long* rows = l.rows + kb_row_in_block(0, max_tasks);
+            KB_TRY(hipMemcpy2DAsync(rows, rowlen * sizeof(long long), dcost, sizeof(long long), sizeof(long long), k,
+                                    hipMemcpyDeviceToDevice, st));
+            KB_TRY(hipMemcpy2DAsync(rows + 1, rowlen * sizeof(long long), dflow, sizeof(long long), sizeof(long long),
+                                    k, hipMemcpyDeviceToDevice, st));
+            for (size_t i = 0; i < k; ++i) {
+                const size_t t = (size_t)(l.toff[i + 1] - l.toff[i]);
+                if (t)
+                    KB_TRY(hipMemcpyAsync(l.rows + kb_row_in_block(i, max_tasks) + 2, l.scratch + l.toff[i],
+                                          t * sizeof(long long), hipMemcpyDeviceToDevice, st));
+            }
+            KB_TRY(hipMemcpyAsync(doff, l.off.data(), k * sizeof(long long), hipMemcpyHostToDevice, st));
+            if (rc == KS_OK)
                 hipLaunchKernelGGL(k_localize, dim3(std::max<size_t>(1, std::min<size_t>(64, (rowlen + 255) / 256)), k),
                                    dim3(256), 0, st, (int)k, (int)rowlen, (const long long*)doff, l.rows);
-                KB_HIP(hipGetLastError());
-            }
+            KB_TRY(hipGetLastError());
         }
+        KB_TRY(hipStreamSynchronize(st));
         if (rc != KS_OK) {
             status[li] = rc;
             if (first_err.empty()) first_err = "rank " + std::to_string(l.grank) + ": " + c->err;
-            const long long sw = rc;
-            KB_HIP(hipMemcpyAsync(l.rows, &sw, sizeof(long long), hipMemcpyHostToDevice, st));
+            // the status word goes out in the block when the rows buffer exists
+            if (l.rows) {
+                const long long sw = rc;
+                (void)hipMemcpy(l.rows, &sw, sizeof(long long), hipMemcpyHostToDevice);
+            }
         }
-        KB_HIP(hipStreamSynchronize(st));
+#undef KB_TRY
     }
     // 2. every rank learns whether any rank failed (min over the status words), so
     //    all of them return the same error instead of only the failing one
     if (b->world > 1) {
         for (size_t li = 0; li < b->loc.size(); ++li) {
             auto& l = b->loc[li];
-            KB_HIP(hipSetDevice(l.device));
-            if (!l.stat) KB_HIP(hipMalloc(&l.stat, sizeof(long long)));
             const long long sw = status[li];
-            KB_HIP(hipMemcpy(l.stat, &sw, sizeof(long long), hipMemcpyHostToDevice));
+            // (a failure to post the word is itself this rank's failure; it still enters)
+            if ((hipSetDevice(l.device) != hipSuccess ||
+                 hipMemcpy(l.stat, &sw, sizeof(long long), hipMemcpyHostToDevice) != hipSuccess) &&
+                status[li] == KS_OK) {
+                status[li] = KS_E_DEVICE;
+                if (first_err.empty()) first_err = "rank " + std::to_string(l.grank) + ": status word not posted";
+            }
         }
         KB_NCCL(rccl().GroupStart());
         for (auto& l : b->loc)
             KB_NCCL(rccl().AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream()));
         KB_NCCL(rccl().GroupEnd());
         long long worst = 0;
-        for (auto& l : b->loc) {
-            KB_HIP(hipSetDevice(l.device));
+        for (size_t li = 0; li < b->loc.size(); ++li) {
+            auto& l = b->loc[li];
             long long sw = 0;
-            KB_HIP(hipStreamSynchronize(l.ctx->eng.stream()));
-            KB_HIP(hipMemcpy(&sw, l.stat, sizeof(long long), hipMemcpyDeviceToHost));
-            worst = std::min(worst, sw);
+            if (hipSetDevice(l.device) != hipSuccess || hipStreamSynchronize(l.ctx->eng.stream()) != hipSuccess ||
+                hipMemcpy(&sw, l.stat, sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+                sw = KS_E_DEVICE;
+            worst = std::min<long long>(worst, std::min<long long>(sw, status[li]));
         }
         if (worst != 0)
             return b->fail((int)worst, first_err.empty() ? "another rank failed to pack its rows (status " +
                                                                std::to_string(worst) + ")"
                                                          : first_err);
     }
+    // world 1: this process's own failure ends it here (no peer waits)
+    for (int rc : status)
+        if (rc != KS_OK) return b->fail(rc, first_err);
     // 3. one group: every rank's block to global rank 0
     long long* rbuf = nullptr;
     for (auto& l : b->loc)

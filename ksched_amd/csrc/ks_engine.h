@@ -37,6 +37,12 @@ public:
     // of every node it touches plus the raw records; nslots = node slots in use.
     int apply(const NodeEdit* edits, size_t ne, const ks_delta* recs, size_t k, int64_t nslots, std::string& err);
 
+    // The graph is a disjoint union of independent cells: cell i owns the node ids
+    // (off[i], off[i+1]] (k + 1 offsets; no arc may cross two cells). Cells the cell
+    // solver holds are then solved one workgroup each in ONE launch (ks_cell.h);
+    // k = 0 forgets the partition (the whole graph is one cell).
+    void set_cells(const int64_t* off, size_t k);
+
     // Node state changes outside a stream (the auto-sink demand).
     int set_nodes(const NodeEdit* edits, size_t ne, std::string& err);
 

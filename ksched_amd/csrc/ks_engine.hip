@@ -65,6 +65,7 @@
 #include <cstring>
 #include <vector>
 
+#include "ks_cell.h"
 #include "ks_engine.h"
 #include "ks_sched.h"
 
@@ -78,22 +79,10 @@ constexpr int NGC = 6;             // group classes: 4, 8, 16, 32, 64 lanes; 64 
 constexpr int HEAVY_MIN = 4096;    // degree > 4096: hub, chunked over workgroups
 constexpr int CHUNK = 1024;        // heavy hubs: 1024 residual arcs per workgroup
 constexpr int PER_T = CHUNK / 256; // arcs per thread in a hub chunk
-#ifndef KS_HSPLIT
-#define KS_HSPLIT 4                // Bellman-Ford: workgroups per hub chunk (one arc per thread at 4)
-#endif
-constexpr int HSPLIT = KS_HSPLIT;
+constexpr int HSPLIT = 4;          // Bellman-Ford: workgroups per hub chunk (one arc per thread at 4)
 constexpr int BF_PER_T = PER_T / HSPLIT;
 static_assert(PER_T % HSPLIT == 0, "a hub chunk splits into whole arcs per thread");
-#ifndef KS_WPW
-#define KS_WPW 2
-#endif
-constexpr int WPW = KS_WPW;        // windows per wave in sparse (grid-stride) passes
-#ifndef KS_NB
-#define KS_NB 4                    // chunked-node discharge: 64-arc batches in flight per wave
-#endif
-#ifndef KS_CHUNK_BLK
-#define KS_CHUNK_BLK 1             // sweeps: one workgroup per chunked-class node (0: one wave)
-#endif
+constexpr int WPW = 2;             // windows per wave in sparse (grid-stride) passes
 constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
@@ -103,6 +92,7 @@ constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
+constexpr double kCellLimitS = 20.0;       // the cell solver's in-kernel wall-clock limit (every workgroup exits)
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7 };
 constexpr int AUG_KMAX = 4096;     // most excess nodes a tail's walkers start from (ks_opts.tail_nodes)
@@ -114,24 +104,7 @@ constexpr long long FS_NONE = (1LL << FS_PB) - 1;    // no parent (an excess nod
 constexpr long long FS_DMAX = 1LL << 36;             // distances beyond are not searched
 constexpr int FDEF_CAP = 64;       // deficits one forward update traces paths to
 constexpr int FS_LIST_BLOCKS = 128;
-#ifndef KS_FWD_WIDE_OFF
-#define KS_FWD_WIDE_OFF 0          // 1: a wide or overlong search ends a coarse phase's forward updates (0: one global update, then forward again; config 4 -2..4 ms, config 3 never runs them)
-#endif
-#ifndef KS_FWD_UPD
-#define KS_FWD_UPD 4               // forward updates per cycle once a search finished within its rounds (2: ~1 ms slower on config 4)
-#endif
-#ifndef KS_FWD_LAST
-#define KS_FWD_LAST 0              // 1: forward updates in the last phase too (guarded by the rate rule)
-#endif
-#ifndef KS_FWD_EXIT
-#define KS_FWD_EXIT 0              // 1: coarse phases in forward mode end by the global-update rule
-                                   // (measured: draining them is what makes config 4's last phase short)
-#endif
-#ifdef KS_FWD_NOADAPT
-#define KS_FWD_FIXED 1
-#else
-#define KS_FWD_FIXED 0
-#endif
+constexpr int FWD_UPD = 4;         // forward updates per cycle once a search finished within its rounds (2: ~1 ms slower on config 4)
 
 struct Ctl {
     long long eps;
@@ -186,10 +159,8 @@ struct CItem {                     // one 64-arc chunk of a chunked-class node
     int node, begin, end, lead;    // lead = 1 for the node's first chunk
 };
 // A wave owns one window: win_batches(c) batches of 64/G consecutive node ids.
-#ifndef KS_WB_CUT
-#define KS_WB_CUT 4                // classes below this own two batches per window, the rest one
-#endif
-__host__ __device__ constexpr int win_batches(int c) { return c < KS_WB_CUT ? 2 : 1; }
+// classes below 4 (≤ 16 lanes per node) own two batches per window, the rest one
+__host__ __device__ constexpr int win_batches(int c) { return c < 4 ? 2 : 1; }
 static_assert(NGC == 6, "KS_BY_CLASS dispatches six classes");
 __host__ __device__ constexpr int win_slots(int c) { return win_batches(c) * (64 / class_lanes(c)); }
 
@@ -1027,84 +998,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
 // per batch instead of the claim/arrive protocol of hubs.
 // e, px, b0, en: the node's excess, price and segment, loaded by the caller
 // together with its frontier flag (one dependent step fewer).
-template <int NB>
-__device__ void node_discharge(const DG& g, const Front& F, const Front& N, int x, long long e, long long px,
-                               int b0, int en, long long* __restrict__ PN, const long long* __restrict__ P,
-                               long long eps, Pend& pd, int& out, Cnt& c) {
-    const int lane = lane_id();
-    if (lane == 0) F.flag[x] = 0;   // the lead consumes the node's flag
-    if (e <= 0) return;
-    if (lane == 0) c.visit++;
-    long long rem = e, minc = INF64;
-    for (int base = b0; base < en; base += 64 * NB) {
-        long long r[NB], cs[NB], pw[NB], uc[NB];
-        int w[NB], rv[NB];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int a = base + j * 64 + lane;
-            r[j] = 0;
-            cs[j] = 0;
-            w[j] = 0;
-            rv[j] = 0;
-            uc[j] = 0;
-            if (a < en) {   // the whole record: a push needs no further load
-                const Pos q = ld_pos(g.pos + a);
-                r[j] = q.rcap;
-                w[j] = q.head;
-                cs[j] = q.cost;
-                rv[j] = q.rev;
-                uc[j] = q.ucap;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) pw[j] = (base + j * 64 + lane < en) ? P[ni(w[j])] : 0;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int a = base + j * 64 + lane;
-            const bool valid = a < en;
-            const long long cr = cs[j] + px - pw[j];
-            const long long adm = (valid && cr < 0 && r[j] > 0) ? r[j] : 0;
-            long long d = 0;
-            if (rem > 0) {   // wave-uniform
-                const long long incl = wave_incl_scan(adm, lane);
-                const long long total = __shfl(incl, WAVE - 1);
-                d = rem - (incl - adm);
-                d = d < 0 ? 0 : (d > adm ? adm : d);
-                if (d > 0) {
-                    push_arc(g, &N, a, w[j], r[j], d, pd, out, rv[j], uc[j]);
-                    c.push++;
-                }
-                rem -= total < rem ? total : rem;
-            }
-            if (valid) {
-                c.scan++;
-                if (cr < 0) {
-                    if (r[j] - d > 0) minc = min(minc, cr);
-                } else if (r[j] > 0 || cr <= eps) {
-                    minc = min(minc, cr);
-                }
-            }
-        }
-        flush_pending(g, &N, pd, out);
-        if (rem == 0) break;   // no relabel needed: the rest of the arcs need no scan
-    }
-    minc = wave_min(minc);
-    if (lane == 0) {
-        const long long pushed = e - rem;
-        if (pushed) atom_add(&g.excess[x], -pushed);
-        long long np = px;
-        if (rem > 0) {
-            if (minc >= INF64) g.ctl->infeasible = 1;
-            else np = px - (minc + eps);
-            c.relabel++;
-            N.flag[x] = 1;
-            out = 1;
-        }
-        PN[ni(x)] = np;
-    }
-}
-
-// Whole-node discharge by one workgroup (chunked class; KS_CHUNK_BLK): 512 arcs
+// Whole-node discharge by one workgroup (chunked class): 512 arcs
 // per pass (two per thread, all loads issued together), the excess distributed
 // by one block-wide scan. A rack (≈ 440 arcs) is one pass — with one wave per
 // node it took two dependent batches, and the chunked node was the last block
@@ -1208,13 +1102,10 @@ __device__ __forceinline__ int class_of_window(const DG& g, int w) {
 struct WinFlag {
     int slot;        // flag index this lane read (-1: none)
     int raw;         // the flag byte
-    long long a;     // KS_PREFETCH, class windows: loaded WITH the flag — sweeps: the node's
+    long long a;     // class windows: loaded WITH the flag — sweeps: the node's
     long long p;     //   excess and price (read buffer); Bellman-Ford: its distance and p0;
     long long seg;   //   both: its packed segment bounds (one dependent step fewer per launch)
 };
-#ifndef KS_PREFETCH
-#define KS_PREFETCH 1
-#endif
 // MODE 0: the flag only; 1: sweep (excess, P); 2: Bellman-Ford (dist, p0).
 template <int MODE>
 __device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char* flags, int w,
@@ -1234,7 +1125,7 @@ __device__ __forceinline__ WinFlag window_load(const DG& g, const unsigned char*
                 ws = win_slots(k);
             }
         if (ln < ws) f.slot = ob + (w - wb) * ws + ln;
-        if (KS_PREFETCH && MODE && f.slot >= 0) {
+        if (MODE && f.slot >= 0) {
             f.seg = g.p0[ni(f.slot) + ND_SEG];
             if (MODE == 1) {
                 f.a = atom_load(&g.excess[f.slot]);
@@ -1288,13 +1179,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
         long long e = 0, pv = 0;
         int b0 = 0, en = 0;
-        if (KS_PREFETCH) {
-            window_node(f, v, base, e, pv, b0, en);
-        } else if (v >= 0) {
-            e = atom_load(&g.excess[v]);
-            pv = P[ni(v)];
-            seg_of(g.p0, v, b0, en);
-        }
+        window_node(f, v, base, e, pv, b0, en);
         if (v < 0) e = 0;
         sweep_group<G>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
@@ -1359,10 +1244,9 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
 #endif
         }
     } else if ((int)blockIdx.x >= g.nhitems + g.sw_clsb) {
-        // chunked class: one workgroup per node (KS_CHUNK_BLK) or one wave per node,
-        // so no wave serialises two of them
-        const int i = KS_CHUNK_BLK ? (int)blockIdx.x - g.nhitems - g.sw_clsb
-                                   : ((int)blockIdx.x - g.nhitems - g.sw_clsb) * WPB + (int)(threadIdx.x >> 6);
+        // chunked class: one workgroup per node (a wave per node made the chunked
+        // node the last block of almost every sweep)
+        const int i = (int)blockIdx.x - g.nhitems - g.sw_clsb;
         if (i < g.ncls_c) {
             const int x = g.obeg[CCLS] + i;
             // flag, excess and record (price, segment) issued together
@@ -1374,24 +1258,17 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(e), "v"(px), "v"(sw));
             const int b0 = (int)(unsigned)((unsigned long long)sw & 0xffffffffULL);
             const int en = (int)(unsigned)((unsigned long long)sw >> 32);
-            if (KS_CHUNK_BLK) {
-                // the flag and the excess may change under the block's feet (pushes into
-                // x, the flag cleared by thread 0): thread 0's reading decides for all
-                __shared__ long long s_e;
-                __shared__ int s_go;
-                if (threadIdx.x == 0) {
-                    s_e = e;
-                    s_go = c_done && c_act && fl;
-                }
-                __syncthreads();
-                if (s_go) {
-                    node_discharge_blk(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
-#ifdef KS_STAMPS
-                    kind = 2;
-#endif
-                }
-            } else if (c_done && c_act && fl) {
-                node_discharge<KS_NB>(g, F, N, x, e, px, b0, en, PN, P, eps, pd, out, c);
+            // the flag and the excess may change under the block's feet (pushes into
+            // x, the flag cleared by thread 0): thread 0's reading decides for all
+            __shared__ long long s_e;
+            __shared__ int s_go;
+            if (threadIdx.x == 0) {
+                s_e = e;
+                s_go = c_done && c_act && fl;
+            }
+            __syncthreads();
+            if (s_go) {
+                node_discharge_blk(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
 #ifdef KS_STAMPS
                 kind = 2;
 #endif
@@ -1484,17 +1361,7 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 
 // Relax the in-arcs of a low-degree node u (≤ 8 arcs: tasks, PUs) right after
 // its distance dropped to du: a second hop inside the same round.
-#ifndef KS_HOP3
-#define KS_HOP3 0
-#endif
-#ifndef KS_HUB_LAZY
-#define KS_HUB_LAZY 0              // 1: hub chunks test the residual before the tail gathers (measured: no faster)
-#endif
 template <bool PR>
-__device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
-                           long long B, long long* hub_min, int& out);
-
-template <bool PR, bool MID = (KS_HOP3 != 0)>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
                                             int b0, int b1, long long eps, long long B, long long* hub_min, int& out) {
     // the records of all (≤ 8) arcs issued together; usually one in-arc carries
@@ -1537,77 +1404,19 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
         const long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
         if (offer<PR>(g, nf, u2, cand, du2, B, hub_min, out)) {
-            if (MID && u2 >= g.obeg[2] && u2 < g.obeg[4]) {
-                expand_mid<PR>(g, nf, u2, cand, pu2, eps, B, hub_min, out);   // a machine: two more hops
-            } else {
-                nf.flag[u2] = 1;
-                out = 1;
-            }
-        }
-    }
-}
-
-// KS_HOP3: a mid-degree node (≤ 32 arcs: machines) reached through a leaf relaxes
-// its own in-arcs at once, and the leaves it lowers (tasks) theirs: an alternating
-// machine ← task ← machine ← task path advances two displacements per round.
-template <bool PR>
-__device__ void expand_mid(const DG& g, const Front& nf, int u, long long du, long long pu, long long eps,
-                           long long B, long long* hub_min, int& out) {
-    int b0, b1;
-    seg_of(g.p0, u, b0, b1);
-    for (int base = b0; base < b1; base += 8) {
-        unsigned live = 0;
-        int hd[8];
-        long long cb[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            hd[k] = 0;
-            cb[k] = 0;
-            if (base + k < b1) {
-                const Pos q = ld_pos(g.pos + base + k);
-                hd[k] = q.head;
-                cb[k] = q.cost;
-                if (q.ucap - q.rcap > 0) live |= 1u << k;
-            }
-        }
-        while (live) {
-            const int k = __builtin_ctz(live);
-            live &= live - 1;
-            int u3 = 0;
-            long long c3 = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j == k) {
-                    u3 = hd[j];
-                    c3 = cb[j];
-                }
-            const long long pu3 = g.p0[ni(u3)];
-            const long long du3 = u3 < g.hub_base ? g.dist[ni(u3)] : INF64;
-            const long long cand = du + arc_len<PR>(pu3, c3, pu, eps);
-            if (!offer<PR>(g, nf, u3, cand, du3, B, hub_min, out)) continue;
-            if (g.expand && u3 < g.obeg[2]) {
-                int e0, e1;
-                seg_of(g.p0, u3, e0, e1);
-                expand_leaf<PR, false>(g, nf, u3, cand, pu3, e0, e1, eps, B, hub_min, out);
-            } else {
-                nf.flag[u3] = 1;
-                out = 1;
-            }
+            nf.flag[u2] = 1;
+            out = 1;
         }
     }
 }
 
 // Relax in-arc (u→v) = reverse of CSR arc a = (v→u); residual ucap − rcap,
 // cost −cost(a). Loads are issued before the residual test (short chain).
-// LAZY: test the residual before gathering the tail's record (hub chunks: a
-// hub's in-arcs are mostly saturated, and their gathers are most of a heavy
-// round's bytes; elsewhere the gathers issue with the arc for a shorter chain).
-template <bool PR, bool LAZY = false>
+template <bool PR>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
                                          long long eps, long long B, long long* hub_min, int& out) {
     const Pos q = ld_pos(g.pos + a);
     const long long rin = q.ucap - q.rcap;
-    if (LAZY && rin <= 0) return;
     const int u = q.head;
     const long long ca = q.cost;
     const long long pu = g.p0[ni(u)];
@@ -1657,13 +1466,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         const int v = mm ? base + __ffsll((long long)mm) - 1 : -1;
         long long d = INF64, pv = 0;
         int b0 = 0, en = 0;
-        if (KS_PREFETCH) {
-            window_node(f, v, base, d, pv, b0, en);
-        } else if (v >= 0) {
-            d = atom_load(&g.dist[ni(v)]);
-            pv = g.p0[ni(v)];
-            seg_of(g.p0, v, b0, en);
-        }
+        window_node(f, v, base, d, pv, b0, en);
         if (v < 0) d = INF64;
         bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
@@ -1756,7 +1559,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR, KS_HUB_LAZY != 0>(g, N, a, dv, pv, eps, B, hub_min, out);
+                        relax_in<PR>(g, N, a, dv, pv, eps, B, hub_min, out);
                         scans++;
                     }
                 }
@@ -2403,7 +2206,7 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
             if (width > g.ctl->fs_maxcnt) g.ctl->fs_maxcnt = width;
             // a frontier this wide (a hub's arcs in reach) costs more per unit than
             // the global update it replaces: fail the search as wide
-            if (width > g.fs_wide && !KS_FWD_FIXED) g.ctl->fs_fail = 2;
+            if (width > g.fs_wide) g.ctl->fs_fail = 2;
         }
     }
     if (done) return;
@@ -2457,6 +2260,10 @@ __global__ void k_fs_apply(DG g) {
         return;
     }
     const long long eps = g.ctl->eps;
+    if (D > (1LL << 60) / eps) {   // ε·D would overflow the prices: a backward update instead
+        if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->fs_fail = 1;
+        return;
+    }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
         const long long d = fs_dist(atom_load(&g.dist[ni(v)]));
         if (d < D) {
@@ -2950,7 +2757,11 @@ struct EngineImpl {
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     hipEvent_t kev[4] = {};   // kernel-batch timing (price refinement)
-    hipEvent_t cev[CYC_SLOTS][2] = {};  // per-cycle timing: after the BF rounds, after the apply
+    // per-cycle timing, each kind's span bracketing exactly its kernels: [0] before the
+    // first Bellman-Ford round, [1] after the last, [2] before the first sweep, [3] after
+    // the last sweep; forward cycles: [0]/[1] around each update's search rounds (fev)
+    hipEvent_t cev[CYC_SLOTS][4] = {};
+    hipEvent_t fev[CYC_SLOTS][8] = {};
     hipEvent_t cdone[CYC_SLOTS] = {};   // a cycle's control snapshot has landed (timed: cycle end)
     hipEvent_t cstart = nullptr;        // start of a phase's first cycle
     Ctl* h_cyc[CYC_SLOTS] = {};         // pinned control snapshots of the cycles in flight
@@ -3024,6 +2835,16 @@ struct EngineImpl {
     DBuf<unsigned char> map_itype, map_tmp;
     DBuf<uint64_t> map_scratch;  // device vector behind ks_get_task_mapping
     DBuf<ks_flow> flow_recs;
+    // ---- cell solver (ks_cell.h): one workgroup per small graph
+    bool cell_layout = false;           // the CSR was built cell-major (the cell solver's node order)
+    std::vector<int64_t> cell_off;      // node-id partition into independent cells (ks_batch); empty: one
+    std::vector<CellDesc> h_cells;      // per cell: its class bounds in internal ids
+    int cell_max = 0;                   // largest cell (node slots)
+    DBuf<CellDesc> cells;
+    DBuf<int> cl_lists, cl_rln;
+    DBuf<long long> cl_rlp;
+    DBuf<CellOut> cl_out;
+    std::vector<CellOut> h_cell_out;
     // ---- scheduler-side sweeps (ks_sched.hip)
     DBuf<int> sched_i;                  // int scratch
     DBuf<unsigned long long> sched_u;   // u64 scratch
@@ -3076,10 +2897,14 @@ struct EngineImpl {
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
+        cells.release(); cl_lists.release(); cl_rln.release(); cl_rlp.release(); cl_out.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         for (auto* h : h_cyc)
             if (h) (void)hipHostFree(h);
         for (auto& c : cev)
+            for (auto& e : c)
+                if (e) (void)hipEventDestroy(e);
+        for (auto& c : fev)
             for (auto& e : c)
                 if (e) (void)hipEventDestroy(e);
         for (auto& e : cdone)
@@ -3188,7 +3013,7 @@ struct EngineImpl {
     int sweep_cls_blocks() const { return std::max(1, (wbeg[CCLS] + WPW * WPB - 1) / (WPW * WPB)); }
     // sweeps: hub chunks, class-window blocks, one wave per chunked-class node
     int sweep_grid() const {
-        return nhitems + sweep_cls_blocks() + (KS_CHUNK_BLK ? ncls[CCLS] : (ncls[CCLS] + WPB - 1) / WPB);
+        return nhitems + sweep_cls_blocks() + ncls[CCLS];
     }
     int sparse_grid() const {
         return nhitems * HSPLIT + std::max(1, (wbeg[CCLS] + ncitems + WPW * WPB - 1) / (WPW * WPB));
@@ -3224,6 +3049,8 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
     for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
     for (auto& c : s.cev)
+        for (auto& e : c) KS_CHECK(hipEventCreate(&e));
+    for (auto& c : s.fev)
         for (auto& e : c) KS_CHECK(hipEventCreate(&e));
     for (auto& e : s.cdone) KS_CHECK(hipEventCreate(&e));
     KS_CHECK(hipEventCreate(&s.cstart));
@@ -3429,6 +3256,61 @@ void Engine::store_stats(ks_store_stats* o) const {
     o->residual_slots = s.m2cap;
 }
 
+// Cell-major internal ids for the cell solver (ks_cell.h): every cell (a ks_batch
+// graph, or the whole graph) is one contiguous id range, its nodes grouped by the
+// cell solver's degree classes (cell_class of the segment capacity). Slots past the
+// partition belong to the last cell. Computed on the host from the capacities.
+static int cell_order(EngineImpl& s, int64_t ncap, std::string& err) {
+    hipStream_t st = s.stream;
+    std::vector<int> capv(ncap);
+    if (ncap) KS_CHECK(hipMemcpyAsync(capv.data(), s.capv.p, ncap * sizeof(int), hipMemcpyDeviceToHost, st));
+    KS_CHECK(hipStreamSynchronize(st));
+    const size_t k = s.cell_off.size() >= 2 ? s.cell_off.size() - 1 : 1;
+    std::vector<int64_t> bound(k + 1, 0);   // slot bounds of each cell
+    for (size_t i = 1; i < k; ++i) bound[i] = std::min<int64_t>(ncap, std::max<int64_t>(0, s.cell_off[i]));
+    bound[k] = ncap;
+    std::vector<int> cnt(k * CELL_NCLS, 0);
+    std::vector<unsigned char> cls(ncap);
+    for (size_t c = 0; c < k; ++c)
+        for (int64_t v = bound[c]; v < bound[c + 1]; ++v) {
+            cls[v] = (unsigned char)cell_class(capv[v]);
+            ++cnt[c * CELL_NCLS + cls[v]];
+        }
+    s.h_cells.assign(k, CellDesc{});
+    std::vector<int> next(k * CELL_NCLS);
+    int o = 0, mx = 0;
+    for (size_t c = 0; c < k; ++c) {
+        const int b = o;
+        for (int q = 0; q < CELL_NCLS; ++q) {
+            s.h_cells[c].cb[q] = o;
+            next[c * CELL_NCLS + q] = o;
+            o += cnt[c * CELL_NCLS + q];
+        }
+        s.h_cells[c].cb[CELL_NCLS] = o;
+        mx = std::max(mx, o - b);
+    }
+    std::vector<int> perm(ncap);
+    for (size_t c = 0; c < k; ++c)
+        for (int64_t v = bound[c]; v < bound[c + 1]; ++v) perm[v] = next[c * CELL_NCLS + cls[v]]++;
+    if (ncap) KS_CHECK(hipMemcpyAsync(s.perm.p, perm.data(), ncap * sizeof(int), hipMemcpyHostToDevice, st));
+    s.cell_max = mx;
+    for (int c = 0; c <= NGC; ++c) s.ncls[c] = 0;
+    for (int c = 0; c <= NGC; ++c) s.obeg[c] = s.wbeg[c] = 0;
+    for (int c = 0; c < NGC; ++c) s.oend[c] = 0;
+    s.nheavy = 0;
+    s.hub_base = (int)ncap;
+    s.nn = (int)ncap;
+    const int nn = (int)ncap;
+    KS_CHECK(s.cells.ensure(k));
+    KS_CHECK(hipMemcpyAsync(s.cells.p, s.h_cells.data(), k * sizeof(CellDesc), hipMemcpyHostToDevice, st));
+    KS_CHECK(s.cl_lists.ensure(2 * (size_t)std::max(nn, 1)));
+    KS_CHECK(s.cl_rln.ensure(std::max(nn, 1)));
+    KS_CHECK(s.cl_rlp.ensure(std::max(nn, 1)));
+    KS_CHECK(s.cl_out.ensure(k));
+    s.h_cell_out.resize(k);
+    return KS_OK;
+}
+
 // ------------------------------------------------------------------ build ---
 static int build(EngineImpl& s, std::string& err) {
     hipStream_t st = s.stream;
@@ -3455,45 +3337,50 @@ static int build(EngineImpl& s, std::string& err) {
                        (const int*)s.deg.p, (const unsigned char*)s.n_alive.p, (const unsigned char*)s.n_type.p,
                        s.incremental ? 1 : 0, s.n_hint.p,
                        s.n_grow.p, s.capv.p, s.cls.p);
-    {
-        hipcub::CountingInputIterator<int> it(0);
-        size_t tmp = 0, t2 = 0;
-        for (unsigned char c = 0; c <= NGC; ++c) {
-            KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
-                                              ClassIs{s.cls.p, c}, st));
-            tmp = std::max(tmp, t2);
+    if (s.cell_layout) {
+        int rc = cell_order(s, ncap, err);   // perm, cell descriptors; no lane-group classes or hubs
+        if (rc) return rc;
+    } else {
+        {
+            hipcub::CountingInputIterator<int> it(0);
+            size_t tmp = 0, t2 = 0;
+            for (unsigned char c = 0; c <= NGC; ++c) {
+                KS_CHECK(hipcub::DeviceSelect::If(nullptr, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
+                                                  ClassIs{s.cls.p, c}, st));
+                tmp = std::max(tmp, t2);
+            }
+            KS_CHECK(s.sel_tmp.ensure(tmp));
+            for (unsigned char c = 0; c <= NGC; ++c) {
+                t2 = tmp;
+                KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
+                                                  ClassIs{s.cls.p, c}, st));
+            }
         }
-        KS_CHECK(s.sel_tmp.ensure(tmp));
-        for (unsigned char c = 0; c <= NGC; ++c) {
-            t2 = tmp;
-            KS_CHECK(hipcub::DeviceSelect::If(s.sel_tmp.p, t2, it, s.cls_list[c].p, s.nsel.p + c, (int)ncap,
-                                              ClassIs{s.cls.p, c}, st));
+        KS_CHECK(hipMemcpyAsync(s.ncls, s.nsel.p, (NGC + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipStreamSynchronize(st));
+        s.nheavy = s.ncls[NGC];
+        // 2. internal ids: classes in order, each padded to whole 64-node blocks, hubs last
+        {
+            int o = 0, wv = 0;
+            for (int c = 0; c < NGC; ++c) {
+                s.obeg[c] = o;
+                s.oend[c] = o + s.ncls[c];
+                s.wbeg[c] = wv;
+                const int pad = (s.ncls[c] + 63) / 64 * 64;
+                o += pad;
+                wv += pad / win_slots(c);
+            }
+            s.obeg[NGC] = o;
+            s.wbeg[NGC] = wv;
+            s.hub_base = o;
+            s.nn = o + s.nheavy;
         }
-    }
-    KS_CHECK(hipMemcpyAsync(s.ncls, s.nsel.p, (NGC + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
-    KS_CHECK(hipStreamSynchronize(st));
-    s.nheavy = s.ncls[NGC];
-    // 2. internal ids: classes in order, each padded to whole 64-node blocks, hubs last
-    {
-        int o = 0, wv = 0;
-        for (int c = 0; c < NGC; ++c) {
-            s.obeg[c] = o;
-            s.oend[c] = o + s.ncls[c];
-            s.wbeg[c] = wv;
-            const int pad = (s.ncls[c] + 63) / 64 * 64;
-            o += pad;
-            wv += pad / win_slots(c);
-        }
-        s.obeg[NGC] = o;
-        s.wbeg[NGC] = wv;
-        s.hub_base = o;
-        s.nn = o + s.nheavy;
+        for (int c = 0; c <= NGC; ++c)
+            if (s.ncls[c])
+                hipLaunchKernelGGL(k_make_perm, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c],
+                                   c < NGC ? s.obeg[c] : s.hub_base, (const int*)s.cls_list[c].p, s.perm.p);
     }
     const int nn = s.nn;
-    for (int c = 0; c <= NGC; ++c)
-        if (s.ncls[c])
-            hipLaunchKernelGGL(k_make_perm, dim3(grid_for(s.ncls[c])), dim3(BLK), 0, st, s.ncls[c],
-                               c < NGC ? s.obeg[c] : s.hub_base, (const int*)s.cls_list[c].p, s.perm.p);
     KS_CHECK(s.capi.ensure(nn + 1));
     KS_CHECK(s.iperm.ensure(nn + 1));
     KS_CHECK(s.first.ensure(nn + 1));
@@ -3639,6 +3526,35 @@ static int cold_reset(EngineImpl& s, std::string& err) {
                            (const long long*)s.a_low.p, s.excess.p);
     KS_CHECK(hipGetLastError());
     return KS_OK;
+}
+
+void Engine::set_cells(const int64_t* off, size_t k) {
+    EngineImpl& s = *p_;
+    std::vector<int64_t> v;
+    if (off && k) v.assign(off, off + k + 1);
+    if (v != s.cell_off) {
+        s.cell_off.swap(v);
+        if (s.cell_layout) s.csr_valid = false;   // the cells are laid out anew by the next build
+    }
+}
+
+// The cell solver runs when every cell (the ks_batch partition, else the whole
+// graph) fits one workgroup's LDS and ks_opts.cell_nodes allows it. Sizes are node
+// slots as the build lays them out (the current build's, or the next one's).
+static bool want_cells(const EngineImpl& s) {
+    if (s.opts.cell_nodes < 0) return false;
+    const int64_t lim = std::min<int64_t>(cell_max_nodes(), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
+    const int64_t ncap =
+        s.csr_valid ? s.ncap : s.nslots + (s.incremental ? std::max<int64_t>(64, s.nslots / 16) : 0);
+    if (ncap <= 0) return false;
+    const size_t k = s.cell_off.size() >= 2 ? s.cell_off.size() - 1 : 1;
+    int64_t prev = 0;
+    for (size_t i = 1; i <= k; ++i) {
+        const int64_t b = i == k ? ncap : std::min<int64_t>(ncap, std::max<int64_t>(prev, s.cell_off[i]));
+        if (b - prev > lim) return false;
+        prev = b;
+    }
+    return true;
 }
 
 int Engine::set_nodes(const NodeEdit* edits, size_t ne, std::string& err) {
@@ -4006,6 +3922,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     hipStream_t st = s.stream;
     const bool use_warm = warm && s.has_prev;
     s.solved = false;
+    {   // the cell solver's node order, or the multi-kernel engine's (a change rebuilds the CSR)
+        const bool cells_now = want_cells(s);
+        if (cells_now != s.cell_layout) {
+            s.cell_layout = cells_now;
+            s.csr_valid = false;
+        }
+    }
     res.warm_started = use_warm ? 1 : 0;
     res.rebuilt = s.csr_valid ? 0 : 1;
     res.recoveries = 0;
@@ -4109,7 +4032,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const bool use_fwd = o.fwd_nodes >= 0 && s.m2cap < FS_NONE;
     const int fwd_k = o.fwd_nodes > 0 ? (int)o.fwd_nodes : 64;
     int kf = 16;                        // forward rounds enqueued per cycle (adaptive)
-    uint64_t fwd_updates = 0;
+    uint64_t fwd_updates = 0, fs_launches = 0;
     const int alpha = o.alpha >= 2 ? o.alpha : 8;
     int gi_base = o.gu_interval > 0 ? o.gu_interval : 24;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
@@ -4155,7 +4078,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
     }
     uint64_t sweeps = 0, gus = 0, sweep_launches = 0, bf_launches = 0, sweep_kernels = 0, early_exits = 0;
-    double ms_bf_k = 0, ms_sw_k = 0;   // event-timed Bellman-Ford round batches / sweep batches
+    double ms_bf_k = 0, ms_sw_k = 0, ms_fs_k = 0;   // event-timed spans: BF rounds / sweeps / forward rounds
     int phases = 0;
     int kb = 24;                        // Bellman-Ford rounds enqueued per cycle (adaptive)
     int sseq = 0, bseq = 0;             // frontier buffer sequences
@@ -4226,72 +4149,47 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int list = 0;         // the next update lists its excess nodes for the bound (the last apply found ≤ BX_CAP)
         int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
-        bool fwd_off = false; // a forward search ran past its round budget: backward updates for the rest of the phase
         int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
-        // tail progress per mode (excess units routed per ms of device time): once the
-        // last phase's forward updates route fewer than a quarter of the units per ms
-        // the global updates did (measured: the first tail cycle of a phase routes
-        // several times the later ones' rate), it goes back to global updates
-        double rate_ms[2] = {0, 0};
-        long long rate_units[2] = {0, 0};
-        int rate_n[2] = {0, 0};
-        int last_mode = -1;   // mode of the last completed tail cycle (0 backward, 1 forward)
-        double last_ms = 0, acc_ms = 0;
-        long long last_units = 0;
-        // account a completed cycle that found `units` excess units at its start
-        auto account = [&](int mode, bool tail, double ms, long long units) {
-            if (last_mode >= 0) {
-                rate_ms[last_mode] += last_ms;
-                rate_units[last_mode] += std::max(0LL, last_units - units);
-                rate_n[last_mode] += 1;
-            }
-            last_mode = tail ? mode : -1;
-            last_ms = ms;
-            last_units = units;
-        };
-        auto fwd_worse = [&]() {
-            return !may_end_early && rate_n[1] >= 1 && rate_n[0] >= 1 && rate_ms[1] > 0 && rate_ms[0] > 0 &&
-                   4.0 * (double)rate_units[1] / rate_ms[1] < (double)rate_units[0] / rate_ms[0];
-        };
         int rc = KS_OK;
-        // Forward cycle: [init (or continue the pending search)][kf rounds][apply]
-        // [trace][end]; no sweeps (the trace routes the units).
-        // nupd updates back to back in one cycle (one host round trip): an update
-        // whose search has not converged when the next one starts is continued by it.
+        // Forward cycle: nupd × [init (or continue the pending search)][kf rounds][apply]
+        // [trace][end], then the cycle end; no sweeps (the trace routes the units). An
+        // update whose search has not converged when the next one starts is continued
+        // by it. fev brackets each update's search rounds (the forward kind's time).
         auto enqueue_fwd = [&](int par, int nupd) -> hipError_t {
             hipError_t e = hipSuccess;
             for (int u = 0; u < nupd; ++u) {
                 hipLaunchKernelGGL(k_fs_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+                if ((e = hipEventRecord(s.fev[par][2 * u], st)) != hipSuccess) return e;
                 for (int r = 0; r < kf; ++r) {
                     hipLaunchKernelGGL(k_fs_round, dim3(fsgrid), dim3(BLK), 0, st, g, bseq);
                     ++bseq;
-                    ++bf_launches;
+                    ++fs_launches;
                 }
-                if (u == 0 && (e = hipEventRecord(s.cev[par][0], st)) != hipSuccess) return e;
+                if ((e = hipEventRecord(s.fev[par][2 * u + 1], st)) != hipSuccess) return e;
                 hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
                 hipLaunchKernelGGL(k_fs_trace, dim3(FDEF_CAP), dim3(WAVE), 0, st, g);
                 hipLaunchKernelGGL(k_fs_end, dim3(1), dim3(WAVE), 0, st, g);
             }
-            if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
             return hipEventRecord(s.cdone[par], st);
         };
-        int nupd = 1;         // forward updates per cycle (KS_FWD_UPD once a search finished within its rounds)
+        int nupd = 1;         // forward updates per cycle (FWD_UPD once a search finished within its rounds)
         int completed0 = 0;   // fs_completed at the phase's start of forward cycles
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
+        // cev[0..1] bracket the Bellman-Ford rounds, cev[2..3] the sweeps.
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
             hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, list);
+            hipError_t e = hipEventRecord(s.cev[par][0], st);
+            if (e != hipSuccess) return e;
             for (int r = 0; r < kb; ++r) {   // sparse from the first round: k_gu_init flags the deficits
                 hipLaunchKernelGGL(k_bf_round<false>, dim3(sgrid), dim3(BLK), 0, st, g, bseq, 0);
                 ++bseq;
                 ++bf_launches;
             }
-            hipError_t e = hipEventRecord(s.cev[par][0], st);
-            if (e != hipSuccess) return e;
+            if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
-            if ((e = hipEventRecord(s.cev[par][1], st)) != hipSuccess) return e;
             if (use_aug) {   // tail: walkers, hub distribution, walkers from what it fed
                 hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
                 if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, walk_sl);
@@ -4300,64 +4198,54 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 for (int wp = 1; wp < walk_passes; ++wp)
                     hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
             }
+            if ((e = hipEventRecord(s.cev[par][2], st)) != hipSuccess) return e;
             for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
+            if ((e = hipEventRecord(s.cev[par][3], st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 0);
             sseq += gi;
             return hipEventRecord(s.cdone[par], st);
         };
         // Cycles run one at a time (enqueueing the next one before reading this
         // one's control block was measured slower: the speculative launches cost
-        // more GPU time than the host's decision gap). Timing: BF = from the
-        // previous cycle's end (or the phase start) to after the BF rounds; sweeps
-        // = from after the apply to the cycle's end.
+        // more GPU time than the host's decision gap).
         if (use_fwd) {   // a phase never continues another phase's forward search
             KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
             KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
             KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_completed, 0, sizeof(int), st));
         }
-        KS_CHECK(hipEventRecord(s.cstart, st));
-        hipEvent_t prev_end = s.cstart;
         int cur = 0;
         for (;;) {
             if (fwd) {
                 KS_CHECK(enqueue_fwd(cur, nupd));
                 KS_CHECK(hipEventSynchronize(s.cdone[cur]));
                 const Ctl* hc = s.h_cyc[cur];
-                const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][0], s.cdone[cur]);
-                ms_bf_k += t_bf;
-                ms_sw_k += t_sw;
-                prev_end = s.cdone[cur];
+                double t_fs = 0;
+                for (int u = 0; u < nupd; ++u) t_fs += ev_ms(s.fev[cur][2 * u], s.fev[cur][2 * u + 1]);
+                ms_fs_k += t_fs;
                 cur ^= 1;
-                acc_ms += t_bf + t_sw;
                 const bool completed = hc->fs_done || hc->fs_fail;
                 if (cycle_log)
-                    std::fprintf(stderr, "fwd cycle phase %d eps %lld updates %d rounds %d bf_ms %.3f tr_ms %.3f units %lld n_exc %d done %d fail %d D %lld deficits %d moved %d width %d\n",
-                                 phases, eps_ph, nupd, hc->fs_rounds, t_bf, t_sw, hc->u_exc_rep, hc->n_exc_rep,
+                    std::fprintf(stderr, "fwd cycle phase %d eps %lld updates %d rounds %d fs_ms %.3f units %lld n_exc %d done %d fail %d D %lld deficits %d moved %d width %d\n",
+                                 phases, eps_ph, nupd, hc->fs_rounds, t_fs, hc->u_exc_rep, hc->n_exc_rep,
                                  hc->fs_done, hc->fs_fail, hc->fs_D < FS_DMAX ? hc->fs_D : -1LL, hc->n_fdef,
                                  hc->fs_moved_cyc, hc->fs_maxcnt);
                 if (completed && hc->n_exc_rep == 0) break;   // no excess left: the phase is done
-                if (completed) {
-                    account(1, true, acc_ms, hc->u_exc_rep);
-                    acc_ms = 0;
-                }
                 const int done_now = hc->fs_completed - completed0;
                 completed0 = hc->fs_completed;
                 gus += done_now;
                 fwd_updates += done_now;
                 bool wide = hc->fs_fail == 2;
-                if (!completed && hc->fs_rounds >= fwd_budget && !KS_FWD_FIXED) {
+                if (!completed && hc->fs_rounds >= fwd_budget) {
                     // longer than two global updates: drop it like a wide one
                     KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
                     KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
                     wide = true;
                 }
                 if (hc->fs_fail || wide) {
-                    // list overflow or no deficit in range: one global update; a wide search
-                    // (a hub's arcs in reach: a forward update then costs more per unit than
-                    // a global one): global updates for the rest of the phase
+                    // list overflow, no deficit in range, or a search too wide or too long
+                    // (a hub's arcs in reach): ONE global update, then forward again
                     fwd = 0;
                     fwd_block = 1;
-                    fwd_off = fwd_off || (wide && (!may_end_early || KS_FWD_WIDE_OFF));
                     nupd = 1;
                     continue;
                 }
@@ -4367,12 +4255,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     continue;
                 }
                 kf = std::max(8, std::min(256, hc->fs_rounds + 4));
-                nupd = KS_FWD_UPD;
-                if (!KS_FWD_FIXED && fwd_worse()) {
-                    fwd = 0;
-                    fwd_off = true;
-                    continue;
-                }
+                nupd = FWD_UPD;
                 if (hc->fs_moved_cyc == 0) {
                     fwd = 0;
                     fwd_block = 1;
@@ -4388,11 +4271,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_CHECK(hipEventSynchronize(s.cdone[cur]));
             const Ctl* hc = s.h_cyc[cur];
             sweep_kernels += gi;
-            const double t_bf = ev_ms(prev_end, s.cev[cur][0]), t_sw = ev_ms(s.cev[cur][1], s.cdone[cur]);
-            ms_bf_k += t_bf;   // init + BF rounds
-            ms_sw_k += t_sw;   // sweeps + cycle end
-            prev_end = s.cdone[cur];
-            acc_ms += t_bf + t_sw;
+            const double t_bf = ev_ms(s.cev[cur][0], s.cev[cur][1]), t_sw = ev_ms(s.cev[cur][2], s.cev[cur][3]);
+            ms_bf_k += t_bf;   // BF rounds only
+            ms_sw_k += t_sw;   // sweeps only
             if (hc->infeasible) {
                 rc = KS_E_INFEASIBLE;
                 std::memcpy(s.h_ctl, hc, sizeof(Ctl));
@@ -4416,41 +4297,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
                 std::fprintf(stderr, "\n");
             }
-#ifdef KS_DUMP
-            // diagnostic builds: the residual state at the first tail cycle of a final
-            // phase (tools/proto/tail_dump.c reads it)
-            if (!may_end_early && hc->n_exc > 0 && hc->n_exc <= g.aug_k) {
-                static int dumped = 0;
-                const char* path = std::getenv("KS_DUMP");
-                if (path && !dumped++) {
-                    (void)hipStreamSynchronize(st);
-                    const long long nposn = s.m2cap, nnode = nn, nh = s.nheavy;
-                    std::vector<Pos> hp(nposn);
-                    std::vector<long long> hnd(4 * (size_t)nnode), hex(nnode), hib((size_t)nh * SHARDS);
-                    std::vector<int> hf(nnode + 1);
-                    (void)hipMemcpy(hp.data(), s.pos.p, nposn * sizeof(Pos), hipMemcpyDeviceToHost);
-                    (void)hipMemcpy(hnd.data(), s.nd.p, hnd.size() * 8, hipMemcpyDeviceToHost);
-                    (void)hipMemcpy(hex.data(), s.excess.p, hex.size() * 8, hipMemcpyDeviceToHost);
-                    (void)hipMemcpy(hf.data(), s.first.p, hf.size() * 4, hipMemcpyDeviceToHost);
-                    if (nh) (void)hipMemcpy(hib.data(), s.inbox.p, hib.size() * 8, hipMemcpyDeviceToHost);
-                    for (long long h = 0; h < nh; ++h)
-                        for (int k = 0; k < SHARDS; ++k) hex[s.hub_base + h] += hib[h * SHARDS + k];
-                    if (FILE* f = std::fopen(path, "wb")) {
-                        const long long hdr[6] = {nnode, (long long)s.hub_base, nposn, eps_ph, mult, (long long)hc->n_exc};
-                        std::fwrite(hdr, 8, 6, f);
-                        std::fwrite(hf.data(), 4, hf.size(), f);
-                        std::fwrite(hnd.data(), 8, hnd.size(), f);
-                        std::fwrite(hex.data(), 8, hex.size(), f);
-                        std::fwrite(hp.data(), sizeof(Pos), hp.size(), f);
-                        std::fclose(f);
-                        std::fprintf(stderr, "KS_DUMP: wrote %s (n %lld, positions %lld, eps %lld)\n", path, nnode,
-                                     nposn, eps_ph);
-                    }
-                }
-            }
-#endif
-            account(0, hc->n_exc <= fwd_k, acc_ms, hc->u_exc);
-            acc_ms = 0;
             kb = std::max(kb_min, std::min(256, hc->bf_count - hc->bf_r0 + kb_margin));
             fwd_budget = std::max(16, 2 * (hc->bf_count - hc->bf_r0));
             ++gus;
@@ -4471,8 +4317,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
-            fwd = use_fwd && (may_end_early || KS_FWD_LAST) && !fwd_off && !fwd_block && hc->n_exc > 0 &&
-                  hc->n_exc <= fwd_k;
+            // forward tail updates only in coarse phases: in the last phase config 3's
+            // searches reach the cluster aggregator and widen
+            fwd = use_fwd && may_end_early && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
             fwd_block = 0;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
@@ -4505,7 +4352,84 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
     }
 
-    do {
+    // ---- the cell solver (ks_cell.h): every cell's whole solve in one workgroup,
+    // one launch for all cells; per-cell status and counters come back in CellOut
+    const int ncells = (int)s.h_cells.size();
+    const long long eps_cells = eps;   // ε before the first phase's division (as the loop below)
+    double ms_cell = 0;
+    unsigned long long cell_ctr[5] = {0, 0, 0, 0, 0};   // scans, visits, pushes, relabels, gu scans
+    unsigned long long cell_rounds = 0, cticks_max = 0, cticks_sum = 0;
+    auto run_cells = [&](int mode) -> int {
+        CellArgs a{};
+        a.pos = s.pos.p;
+        a.nd = s.nd.p;
+        a.excess = s.excess.p;
+        a.cells = s.cells.p;
+        a.ncells = ncells;
+        a.nn = nn;
+        a.lists = s.cl_lists.p;
+        a.rl_node = s.cl_rln.p;
+        a.rl_p = s.cl_rlp.p;
+        a.out = s.cl_out.p;
+        a.mult = mult;
+        a.eps_start = eps_cells;
+        a.sat_thr0 = warm_thr;
+        a.warm = use_warm ? 1 : 0;
+        a.alpha = alpha;
+        a.pr_div = (int)pr_div;
+        a.use_pr = use_pr ? 1 : 0;
+        a.pr_cap = pr_cap;
+        a.gi = gi_base;
+        a.phase_exit = phase_exit;
+        a.phase_frac = phase_frac;
+        a.mode = mode;
+        a.max_nodes = s.cell_max;
+        a.timeout_ticks = (unsigned long long)(kCellLimitS * 1e8);
+        KS_CHECK(hipEventRecord(s.kev[2], st));
+        KS_CHECK(cell_launch(a, st));
+        KS_CHECK(hipEventRecord(s.kev[3], st));
+        KS_CHECK(hipMemcpyAsync(s.h_cell_out.data(), s.cl_out.p, ncells * sizeof(CellOut), hipMemcpyDeviceToHost, st));
+        KS_CHECK(hipStreamSynchronize(st));
+        ms_cell += ev_ms(s.kev[2], s.kev[3]);
+        int worst = CS_OK, pmax = 0;
+        for (const CellOut& o : s.h_cell_out) {
+            if (o.status != CS_OK && (worst == CS_OK || worst == CS_INFEASIBLE)) worst = o.status;
+            pmax = std::max(pmax, o.phases);
+            sweeps += o.sweeps;
+            gus += o.updates;
+            cell_rounds += o.bf_rounds;
+            cell_ctr[0] += o.scans;
+            cell_ctr[1] += o.visits;
+            cell_ctr[2] += o.pushes;
+            cell_ctr[3] += o.relabels;
+            cell_ctr[4] += o.gu_scans;
+            cticks_max = std::max<unsigned long long>(cticks_max, o.ticks);
+            cticks_sum += o.ticks;
+        }
+        phases += pmax;
+        return worst;
+    };
+    auto cell_status = [&](int cs, const char* what) -> int {
+        if (cs == CS_OK) return KS_OK;
+        if (cs == CS_INFEASIBLE) {
+            status = KS_E_INFEASIBLE;
+            err = std::string("infeasible: some supply cannot reach a demand node (cell solver, ") + what + ")";
+            return KS_OK;
+        }
+        err = std::string("cell solver did not converge (") + (cs == CS_TIMEOUT ? "wall-clock limit" : "step cap") +
+              ", " + what + ")";
+        return KS_E_DEVICE;
+    };
+    if (s.cell_layout) {
+        KS_CHECK(hipEventRecord(s.ev[3], st));
+        const int cs = run_cells(0);
+        if (cs < 0) return cs;
+        KS_CHECK(hipEventRecord(s.ev[5], st));
+        KS_CHECK(hipEventSynchronize(s.ev[5]));
+        ms_cycles += ev_ms(s.ev[3], s.ev[5]);
+        if (int rc = cell_status(cs, "solve")) return rc;
+        eps = 1;
+    } else do {
         eps = std::max<long long>(1, eps / alpha);
         ++phases;
         // After a failed refinement the flow is feasible and ε-optimal at the old ε:
@@ -4539,7 +4463,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     if (cycle_log)
         std::fprintf(stderr, "solve phases %d updates %llu (forward %llu) early phase ends %llu\n", phases,
                      (unsigned long long)gus, (unsigned long long)fwd_updates, (unsigned long long)early_exits);
-    if (status == KS_E_INFEASIBLE)
+    if (status == KS_E_INFEASIBLE && !s.cell_layout)
         err = "infeasible: some supply cannot reach a demand node (code " + std::to_string(s.h_ctl->infeasible) +
               ", phase " + std::to_string(phases) + ", eps " + std::to_string(eps) + ", updates " +
               std::to_string(gus) + ", sweeps " + std::to_string(sweep_launches) + ")";
@@ -4588,6 +4512,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // conservation violations stay fatal (KS_E_VERIFY).
         for (int attempt = 0; attempt < 2 && bad == 2; ++attempt) {
             ++res.recoveries;
+            if (s.cell_layout) {   // the same repair inside each cell's workgroup
+                const int cs = run_cells(1);
+                if (cs < 0) return cs;
+                if (int rc2 = cell_status(cs, "certificate recovery")) return rc2;
+                if (status != KS_OK) break;
+                rc = verify(&bad);
+                if (rc) return rc;
+                continue;
+            }
             int used = 0;
             const int pr = price_refine(1, &used, 4 * pr_cap);
             if (pr < 0) return pr;
@@ -4617,6 +4550,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     unsigned long long tc[NCTR] = {0};
     for (int i = 0; i < CTR_SHARDS; ++i)
         for (int k = 0; k < NCTR; ++k) tc[k] += hc[i * NCTR + k];
+    if (s.cell_layout) {
+        tc[C_SCAN] += cell_ctr[0];
+        tc[C_VISIT] += cell_ctr[1];
+        tc[C_PUSH] += cell_ctr[2];
+        tc[C_RELABEL] += cell_ctr[3];
+        tc[C_GUSCAN] += cell_ctr[4];
+        tc[C_BFROUND] += cell_rounds;
+    }
     if (cycle_log)
         std::fprintf(stderr, "solve tail walks to a deficit %llu, hops %llu, recoveries %d\n", tc[C_AUGWALK],
                      tc[C_AUGHOP], res.recoveries);
@@ -4658,6 +4599,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.ms_sweep_kernels = ms_sw_k;
     res.gu_launches = bf_launches;
     res.ms_gu_kernels = ms_bf_k;
+    res.fs_launches = fs_launches;
+    res.ms_fs_kernels = ms_fs_k;
+    res.fwd_updates = fwd_updates;
+    res.solver = s.cell_layout ? 1 : 0;
+    res.cells = s.cell_layout ? ncells : 0;
+    res.ms_cell_kernel = ms_cell;
+    res.cell_ticks_max = cticks_max;
+    res.cell_ticks_sum = cticks_sum;
     res.status = status;
     if (status == KS_OK) {
         KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));

@@ -242,6 +242,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
         alive[id - 1] = r.alive ? 1 : 0;
     }
     c->dev_sink_supply = (c->n_sinks == 1) ? c->nodes[c->sink_id].excess : 0;
+    c->eng.set_cells(nullptr, 0);   // a plain load is one graph (ks_batch_load sets its cells after)
     const int rc = c->eng.load((int64_t)maxid, supply.data(), type.data(), alive.data(), arcs, m, c->err);
     c->store_bad = rc != KS_OK;   // the upload failed part-way: nothing may read the store
     return rc;

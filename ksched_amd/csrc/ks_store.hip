@@ -286,11 +286,15 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
             atomicAdd(&d.ctl->updated, 1);
             continue;
         }
-        const int p = claim_pos(d, xs, 2 * s), q = p < 0 ? -1 : claim_pos(d, xd, 2 * s + 1);
+        // both endpoints claim (so a full segment is flagged at each end at once); a
+        // claim that cannot be paired is given back
+        const int p = claim_pos(d, xs, 2 * s), q = claim_pos(d, xd, 2 * s + 1);
         if (p < 0 || q < 0) {
             d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
             if (p < 0) d.n_grow[sl] = 1;
-            else d.n_grow[dl] = 1;
+            if (q < 0) d.n_grow[dl] = 1;
+            if (p >= 0) atomicExch(&d.ent[p], -1);
+            if (q >= 0) atomicExch(&d.ent[q], -1);
             continue;
         }
         d.pos[p].head = xd;

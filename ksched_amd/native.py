@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "ks_batch_load", "ks_batch_solve", "ks_batch_gather",
     "ks_batch_slots", "ks_batch_owner", "ks_batch_block_len", "ks_batch_unpack",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
 
@@ -51,8 +51,8 @@ class KsOpts(C.Structure):
                 ("phase_exit", C.c_int32), ("phase_frac", C.c_int32), ("tail_sweeps", C.c_int32),
                 ("bf_margin", C.c_int32), ("two_hop", C.c_int32), ("log_cycles", C.c_int32),
                 ("fault_inject", C.c_int32), ("walk_passes", C.c_int32), ("tail_nodes", C.c_int32),
-                ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32), ("cell_nodes", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 class KsResult(C.Structure):
@@ -63,10 +63,13 @@ class KsResult(C.Structure):
                 ("ms_phase", C.c_double * 6), ("n_nodes", C.c_int64), ("n_arcs", C.c_int64),
                 ("sweep_launches", C.c_uint64), ("ms_sweep_kernels", C.c_double),
                 ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double), ("warm_started", C.c_int32),
-                ("rebuilt", C.c_int32), ("recoveries", C.c_int32), ("_pad", C.c_int32)]
+                ("rebuilt", C.c_int32), ("recoveries", C.c_int32), ("solver", C.c_int32),
+                ("fs_launches", C.c_uint64), ("ms_fs_kernels", C.c_double), ("fwd_updates", C.c_uint64),
+                ("cells", C.c_int32), ("_pad3", C.c_int32), ("ms_cell_kernel", C.c_double),
+                ("cell_ticks_max", C.c_uint64), ("cell_ticks_sum", C.c_uint64), ("reserved2", C.c_uint64 * 4)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "_pad")}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "_pad3", "reserved2")}
         names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d

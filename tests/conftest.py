@@ -26,8 +26,27 @@ def load_known_answers():
 
 @pytest.fixture(scope="session")
 def ctx():
-    """One HIP solver context shared by the GPU tests (one process on the box)."""
+    """One HIP solver context shared by the GPU tests (one process on the box).
+    Default options: graphs up to the cell solver's size run in one workgroup
+    (ks_cell.hip), larger ones on the multi-kernel engine."""
     from ksched_amd import native
     c = native.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def ctx_engine():
+    """A context pinned to the multi-kernel engine (ks_opts.cell_nodes = -1), so
+    small graphs exercise it too."""
+    from ksched_amd import native
+    c = native.Context(0, cell_nodes=-1)
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["cell", "engine"])
+def any_ctx(request, ctx, ctx_engine):
+    """Each solver path in turn: the default context (cell solver for small
+    graphs) and the engine-pinned one."""
+    return ctx if request.param == "cell" else ctx_engine

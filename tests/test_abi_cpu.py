@@ -32,10 +32,11 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_default_opts():
     lib = native.load()
-    assert lib.ks_abi_version() == native.ABI_VERSION == 2
+    assert lib.ks_abi_version() == native.ABI_VERSION == 3
     o = native.default_opts()
     assert (o.alpha, o.verify, o.auto_sink) == (8, 1, 1)
     assert o.price_refine == 1 and o.gu_interval > 0 and o.warm_start == 0
+    assert o.cell_nodes == 0   # the cell solver on by default for graphs its LDS holds
 
 
 def test_create_fails_loudly_without_device():

@@ -143,7 +143,7 @@ def test_coalesced_stream_solves_like_the_raw_stream():
 def test_config4_full_size_rounds():
     """Config 4 at its stated size: the config-3 cell (100k tasks,
     10k machines, seed 3) under 5 % completions + 5 % arrivals per round, pins,
-    ageing and capacity refresh, five rounds through ks_apply_deltas. Every
+    ageing and capacity refresh, ten rounds through ks_apply_deltas. Every
     round: bit-exact cost vs the cost-scaling oracle on the cell's full graph,
     the oracle's verifier accepts the downloaded flow, and every running task
     stays on its PU (graph_manager.go:675-720 pinning, :803-813 removal)."""
@@ -153,7 +153,7 @@ def test_config4_full_size_rounds():
         ctx.load_graph(cell.graph())
         ctx.solve()
         mp = ctx.task_mapping()
-        for rnd in range(5):
+        for rnd in range(10):
             d = cell.step(mp, done=T // 20, arrive=T // 20)
             ctx.apply_deltas(d)
             r = ctx.solve()
@@ -188,6 +188,51 @@ def test_config5_full_batch_vs_goldens(ctx):
     per = batch.split_costs(u, noff, ctx.flows())
     assert per.tolist() == [gold[s]["cost"] for s in seeds]
     assert r.cost == sum(gold[s]["cost"] for s in seeds)
+    assert r.raw["solver"] == 0                    # one 776k-node graph: the multi-kernel engine
+
+
+def test_config5_cells_one_workgroup_each_vs_goldens():
+    """Config 5 through the C-ABI batch (ks_batch_*): the union's partition is
+    known, so each of the 64 cells is solved by its own workgroup of ONE cell-
+    solver launch (ks_cell.hip); every per-cell cost, flow and task row gathered
+    equals the committed networkx golden, and the mappings are valid."""
+    from conftest import load_goldens
+    T, M, R, J, _ = gen.CONFIGS["config2"]
+    gold = {e["seed"]: e for e in load_goldens() if e["params"] == [T, M, R, J]}
+    seeds = list(range(1000, 1064))
+    graphs = [gen.quincy(T, M, R, J, s) for s in seeds]
+    b = native.Batch(devices=[0])
+    try:
+        b.load(graphs)
+        res = b.solve()
+        assert res[0].raw["solver"] == 1 and res[0].raw["cells"] == 64
+        assert res[0].raw["recoveries"] == 0
+        pu, cost, flow = b.gather(T)
+        assert cost.tolist() == [gold[s]["cost"] for s in seeds]
+        assert flow.tolist() == [gold[s]["flow"] for s in seeds]
+        for i in (0, 17, 63):
+            g = graphs[i]
+            tasks = np.nonzero(g.ntype == 1)[0] + 1
+            check_mapping(g, {int(t): int(p) for t, p in zip(tasks, pu[i]) if p})
+    finally:
+        b.close()
+
+
+def test_batch_gather_pack_failure_returns_error():
+    """ADVICE / VERDICT r3: a rank whose packing fails (here: injected, ks_opts
+    fault_inject bit 2, global rank 0) still reaches the collective point and
+    ks_batch_gather returns the error — no early return, no hang."""
+    graphs = [gen.quincy(1_000, 100, 5, 10, 1300 + i) for i in range(3)]
+    b = native.Batch(devices=[0], fault_inject=4)
+    try:
+        b.load(graphs)
+        b.solve()
+        with pytest.raises(native.KsError) as ei:
+            b.gather(1_000)
+        assert ei.value.code == native.KS_E_DEVICE
+        assert "injected pack failure" in str(ei.value)
+    finally:
+        b.close()
 
 
 def test_deltas_applied_in_place_on_device():
@@ -235,6 +280,7 @@ def test_batch_c_abi_gather_world1():
         b.load(graphs)
         res = b.solve()
         assert len(res) == 1 and res[0].flow == 6 * T
+        assert res[0].raw["solver"] == 1 and res[0].raw["cells"] == 6
         pu, cost, flow = b.gather(T)
         for i, g in enumerate(graphs):
             st, c, f, _ = ko.cost_scaling(g)

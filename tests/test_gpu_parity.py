@@ -41,6 +41,10 @@ def solve_and_check(ctx, g, cost, flow, check_flows=True):
     r = ctx.solve()
     assert r.cost == cost
     assert r.flow == flow
+    # a certificate repair must not hide an ε-optimality bug — no
+    # recovery may run unless a test injects the fault
+    if not ctx.opts.fault_inject:
+        assert r.raw["recoveries"] == 0, "the optimality certificate needed a repair"
     if check_flows:
         fl = flows_by_arc(ctx, g)
         st, c2, _ = ko.verify(g, fl)
@@ -49,7 +53,8 @@ def solve_and_check(ctx, g, cost, flow, check_flows=True):
     return r
 
 
-def test_config1_known_answer(ctx):
+def test_config1_known_answer(any_ctx):
+    ctx = any_ctx
     ka = load_known_answers()["config1"]
     g = gen.trivial(*ka["params"])
     assert (g.n, g.m) == (ka["n"], ka["m"])
@@ -70,9 +75,12 @@ def test_multi_schedule_round1(ctx):
 
 @pytest.mark.parametrize("e", [e for e in load_goldens() if e["m"] <= 60000 and not 1004 <= e["seed"] < 1064],
                          ids=lambda e: f"{e['family']}-{'x'.join(map(str, e['params']))}-s{e['seed']}")
-def test_goldens(ctx, e):
+def test_goldens(any_ctx, e):
+    ctx = any_ctx
     g = gen.trivial(*e["params"]) if e["family"] == "trivial" else gen.quincy(*e["params"], e["seed"])
-    solve_and_check(ctx, g, e["cost"], e["flow"])
+    r = solve_and_check(ctx, g, e["cost"], e["flow"])
+    # which path ran: the cell solver holds every golden up to config-2 size
+    assert r.raw["solver"] == (0 if ctx.opts.cell_nodes < 0 else 1)
     check_mapping(g, ctx.task_mapping())
 
 
@@ -102,13 +110,15 @@ def test_config3_full_size(ctx):
 
 
 # ----------------------------------------------------------------- edge cases ---
-def test_empty_graph(ctx):
+def test_empty_graph(any_ctx):
+    ctx = any_ctx
     ctx.load_arrays(np.zeros(0, native.NODE_DT), np.zeros(0, native.ARC_DT))
     r = ctx.solve()
     assert (r.cost, r.flow) == (0, 0)
 
 
-def test_isolated_nodes_no_arcs(ctx):
+def test_isolated_nodes_no_arcs(any_ctx):
+    ctx = any_ctx
     nodes = [(1, 0, 3), (2, 0, 0), (5, 0, 1)]
     g = graph_from_lists(nodes, np.zeros((0, 5), np.int64))
     ctx.load_graph(g)
@@ -116,7 +126,8 @@ def test_isolated_nodes_no_arcs(ctx):
     assert (r.cost, r.flow) == (0, 0)
 
 
-def test_infeasible_reports_error(ctx):
+def test_infeasible_reports_error(any_ctx):
+    ctx = any_ctx
     # 3 tasks, one PU slot, no unscheduled escape → supply cannot reach the sink
     nodes = [(1, -3, 3), (2, 0, 2), (3, 1, 1), (4, 1, 1), (5, 1, 1)]
     arcs = [(2, 1, 0, 1, 0), (3, 2, 0, 1, 1), (4, 2, 0, 1, 1), (5, 2, 0, 1, 1)]
@@ -127,7 +138,8 @@ def test_infeasible_reports_error(ctx):
     assert ei.value.code == native.KS_E_INFEASIBLE
 
 
-def test_lower_bound_running_arc(ctx):
+def test_lower_bound_running_arc(any_ctx):
+    ctx = any_ctx
     # pinned task: running arc low=1 cap=1 to a PU (graph_manager.go:675-720)
     nodes = [(1, -2, 3), (2, 0, 2), (3, 0, 2), (4, 1, 1), (5, 1, 1), (6, 0, 0)]
     arcs = [(2, 1, 0, 5, 0), (3, 1, 0, 5, 0), (4, 3, 1, 1, 7), (5, 2, 0, 1, 3), (5, 6, 0, 1, 5), (6, 1, 0, 2, 0)]
@@ -138,7 +150,8 @@ def test_lower_bound_running_arc(ctx):
     assert ctx.task_mapping() == {4: 3, 5: 2}
 
 
-def test_random_graphs_vs_oracle(ctx):
+def test_random_graphs_vs_oracle(any_ctx):
+    ctx = any_ctx
     for trial, g in random_graphs(12345, 40):
         st, c, fv, _, _ = ko.ssp(g)
         ctx.load_graph(g)
@@ -284,7 +297,7 @@ def test_tail_walks_do_not_change_the_optimum(opts):
     flow re-verified by the oracle — on a config-2-sized Quincy cell (hub excess
     in every phase's tail) and on random graphs with several deficits, lower
     bounds and parallel paths."""
-    with native.Context(0, **opts) as c2:
+    with native.Context(0, cell_nodes=-1, **opts) as c2:   # the engine's tail (the cell solver has none)
         g = gen.quincy(10_000, 1_000, 25, 100, 2)
         st, c, fv, _, _ = ko.ssp(g)
         assert st == 0
@@ -304,33 +317,40 @@ def test_tail_updates_do_not_change_the_optimum(opts):
     tail), and down to ε = 1 without price refinement; the bounded global update
     off. Same optimum as the oracle, flow re-verified, on a config-2-sized cell
     and random graphs (several deficits, lower bounds, parallel paths)."""
-    with native.Context(0, **opts) as c2:
+    with native.Context(0, cell_nodes=-1, **opts) as c2:   # the engine's tail updates
         g = gen.quincy(10_000, 1_000, 25, 100, 2)
         st, c, fv, _, _ = ko.ssp(g)
         assert st == 0
-        solve_and_check(c2, g, c, fv)
+        fwd = solve_and_check(c2, g, c, fv).raw["fwd_updates"]
         for trial, g in random_graphs(4242, 15):
             st, c, fv, _, _ = ko.ssp(g)
             if st == 0:
-                solve_and_check(c2, g, c, fv)
+                fwd += solve_and_check(c2, g, c, fv).raw["fwd_updates"]
+        # ADVICE r3: the forward update really ran where it is on
+        if opts.get("fwd_nodes", 64) in (64, 4096) and opts.get("bf_bound", 1) >= 0:
+            assert fwd > 0, "no forward tail update ran"
 
 
-@pytest.mark.parametrize("fault", [1, 2])
-def test_failed_certificate_is_recovered(fault):
+@pytest.mark.parametrize("fault,path", [(1, "engine"), (2, "engine"), (2, "cell")])
+def test_failed_certificate_is_recovered(fault, path):
     """A failed final optimality certificate is repaired, not fatal
     (replaces the panic of placement/solver.go:223-225 on a bad solve):
     fault 1 — with price refinement off the ladder runs down to ε = 1 and the
     last phase's walks use the coarse slack (the flow may end 4-optimal only);
     fault 2 — an optimal flow whose prices are perturbed before verification.
     Either way the solve returns the oracle's cost, the flow re-verified, and
-    fault 2 always needs (and counts) a recovery."""
+    fault 2 always needs (and counts) a recovery — on the engine and inside the
+    cell solver's workgroups (its recovery mode: refinement, else one ε = 1 phase)."""
     opts = {"fault_inject": fault}
+    if path == "engine":
+        opts["cell_nodes"] = -1
     if fault == 1:
         opts["price_refine"] = 0
     with native.Context(0, **opts) as c2:
         for g in (gen.quincy(10_000, 1_000, 25, 100, 2), gen.quincy(3_000, 300, 12, 30, 10)):
             st, c, fv, _, _ = ko.ssp(g)
             r = solve_and_check(c2, g, c, fv)
+            assert r.raw["solver"] == (1 if path == "cell" else 0)
             if fault == 2:
                 assert r.raw["recoveries"] >= 1
             assert r.raw["recoveries"] <= 2

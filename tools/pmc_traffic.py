@@ -3,7 +3,9 @@
 calibration run (gpu_calib.sh): per kernel, raw FETCH_SIZE + WRITE_SIZE bytes
 per launch, the calibrated range, and atomic request counts / rates.
 
-    python tools/pmc_traffic.py gpurun_out/<pmc tag> gpurun_out/<calib tag>|<profile.json> DATE > profiles/<tag>_pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/<pmc tag> gpurun_out/<calib tag>|<profile.json> DATE > profiles/<tag>_pmc_<workload>.json
+
+The workload (config2..config5) is the one gpu_pmc.sh profiled (its workload.txt).
 """
 import csv
 import json
@@ -46,12 +48,18 @@ def main():
     if os.path.exists(stats):
         for r in csv.DictReader(open(stats)):
             name = r.get("kernel") or r.get("Name") or ""
-            for key in ("k_sweep", "k_bf_round", "k_saturate"):
+            for key in ("k_sweep", "k_bf_round", "k_saturate", "k_fs_round", "k_cell"):
                 if key + "<" in name or key + "(" in name or name.endswith(key):
                     times.setdefault(key, {"calls": 0, "total_us": 0.0})
                     times[key]["calls"] += int(float(r.get("calls", 0)))
                     times[key]["total_us"] += float(r.get("total_us", 0.0))
-    out = {"date": date, "workload": "config 3 (bench.py --steps 1 --warmup 0): one full solve",
+    wl_path = os.path.join(pmc, "workload.txt")
+    wl = open(wl_path).read().strip() if os.path.exists(wl_path) else "config3"
+    desc = {"config3": "config 3 (bench.py --steps 1 --warmup 0): one full solve",
+            "config2": "config 2 (bench.py --config config2 --steps 3 --warmup 0): three full solves",
+            "config4": "config 4 (bench.py --workload incremental --steps 3 --warmup 0): initial solve + 3 churn rounds",
+            "config5": "config 5 (bench.py --workload batch --steps 1 --warmup 0): warm-up + one batch solve"}[wl]
+    out = {"date": date, "workload": desc, "workload_key": wl,
            "note": "raw = (FETCH_SIZE + WRITE_SIZE) per launch from separate rocprofv3 --pmc passes; gfx950 "
                    "FETCH_SIZE tallies coalesced 4/8-B streams at 1/2 of their bytes and a random 8-B gather at "
                    "64 B (tools/calib/calib_fetch.hip), so the calibrated range is [raw, 2*FETCH + WRITE]; "
