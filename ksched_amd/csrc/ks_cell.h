@@ -52,7 +52,13 @@ struct CellOut {
     int pad[2];
     unsigned long long sweeps, bf_rounds, scans, visits, pushes, relabels, gu_scans;
     unsigned long long ticks;   // s_memrealtime ticks (100 MHz) of the cell's solve
+    // per operation kind (saturate, update init, Bellman-Ford round, update apply,
+    // sweep, refinement init, refinement round, refinement apply): ticks incl. the
+    // barriers and the controller, and counts
+    unsigned long long op_ticks[8];
+    unsigned op_n[8];
 };
+constexpr int CELL_NOPS = 8;
 
 struct CellArgs {
     Pos* pos;

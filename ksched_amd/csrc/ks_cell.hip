@@ -68,9 +68,45 @@ struct K {
     int x0, N, W, maxn;
     int c1, c2, c3, c4, c5, c6;
     long long eps;
+    int eps_shift;        // log2 ε when ε is a power of two (the cell ladder's are), else −1
     int sp;               // sweep parity (pending-relabel buffer)
-    unsigned long long scans, visits, pushes, relabels, guscans;
 };
+
+// Work counters (ks_result units), counted per wave where the work happens: one
+// ballot and, when any lane did work, one LDS add by lane 0 (the ballot must be
+// taken at a point where the whole wave is converged).
+enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, NCTR = 5 };
+__shared__ unsigned long long ctr_[NCTR];
+__device__ __forceinline__ int lane();
+__device__ __forceinline__ void wcount(int i, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m && lane() == 0) atomicAdd(&ctr_[i], (unsigned long long)__popcll(m));
+}
+// Thread-per-node work counts per thread, summed over the wave by DPP (no LDS
+// round trips) and added to the workgroup's counters once per step.
+struct Tc {
+    unsigned c[NCTR] = {0, 0, 0, 0, 0};
+};
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ unsigned dpp_add(unsigned v) {
+    return v + (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {   // the sum lands in lane 63
+    v = dpp_add<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xf>(v);   // row_half_mirror
+    v = dpp_add<0x140, 0xf>(v);   // row_mirror
+    v = dpp_add<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ __forceinline__ void flush(const Tc& t) {
+#pragma unroll
+    for (int i = 0; i < NCTR; ++i) {
+        const unsigned w = wave_sum_u32(t.c[i]);
+        if (lane() == 63 && w) atomicAdd(&ctr_[i], (unsigned long long)w);
+    }
+}
 
 __device__ __forceinline__ long long* prc() { return dyn_; }
 __device__ __forceinline__ int* dst(const K& k) { return reinterpret_cast<int*>(dyn_ + k.maxn); }
@@ -271,7 +307,7 @@ __device__ __forceinline__ void sweep_grp(const CellArgs& A, K& k, int nb, int v
     }
     const bool act = e > 0;
     if (!act) en = b0;
-    if (act && lig == 0) k.visits++;
+    wcount(C_VISIT, act && lig == 0);
     long long rem = e, minc = INF64;
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
     for (int it = 0; it < iters; ++it) {
@@ -286,17 +322,15 @@ __device__ __forceinline__ void sweep_grp(const CellArgs& A, K& k, int nb, int v
             rv = q.rev;
             uc = q.ucap;
             cr = q.cost + pv - P[w - k.x0];
-            k.scans++;
         }
+        wcount(C_SCAN, valid);
         const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
         const long long incl = g_incl_scan<G>(adm);
         const long long total = g_last<G>(incl);
         long long d = rem - (incl - adm);
         d = d < 0 ? 0 : (d > adm ? adm : d);
-        if (d > 0) {
-            push(A, k, nb, a, w, r, d, rv, uc);
-            k.pushes++;
-        }
+        if (d > 0) push(A, k, nb, a, w, r, d, rv, uc);
+        wcount(C_PUSH, d > 0);
         if (valid) {
             if (cr < 0) {
                 if (r - d > 0) minc = min(minc, cr);
@@ -308,13 +342,13 @@ __device__ __forceinline__ void sweep_grp(const CellArgs& A, K& k, int nb, int v
         if (G == 64 && rem == 0) break;
     }
     minc = g_min<G>(minc);
+    wcount(C_RELABEL, act && lig == 0 && rem > 0);
     if (act && lig == 0) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
         if (rem > 0) {
             if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
             else relabel(A, k, v, pv - (minc + k.eps));
-            k.relabels++;
             mark(A, k, nb, v);
         }
     }
@@ -329,7 +363,7 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
     int b0, en;
     seg(A, v, b0, en);
     if (e <= 0) return;
-    if (threadIdx.x == 0) k.visits++;
+    wcount(C_VISIT, threadIdx.x == 0);
     long long rem = e, minc = INF64;
     for (int base = b0; base < en; base += CT) {
         const int a = base + (int)threadIdx.x;
@@ -343,17 +377,15 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
             rv = q.rev;
             uc = q.ucap;
             cr = q.cost + pv - P[w - k.x0];
-            k.scans++;
         }
+        wcount(C_SCAN, valid);
         const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
         long long tot;
         const long long excl = blk_excl_scan(adm, &tot);
         long long d = rem - excl;
         d = d < 0 ? 0 : (d > adm ? adm : d);
-        if (d > 0) {
-            push(A, k, nb, a, w, r, d, rv, uc);
-            k.pushes++;
-        }
+        if (d > 0) push(A, k, nb, a, w, r, d, rv, uc);
+        wcount(C_PUSH, d > 0);
         if (valid) {
             if (cr < 0) {
                 if (r - d > 0) minc = min(minc, cr);
@@ -365,13 +397,13 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
         if (rem == 0) break;
     }
     minc = blk_min(minc);
+    wcount(C_RELABEL, threadIdx.x == 0 && rem > 0);
     if (threadIdx.x == 0) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
         if (rem > 0) {
             if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
             else relabel(A, k, v, pv - (minc + k.eps));
-            k.relabels++;
             mark(A, k, nb, v);
         }
     }
@@ -388,7 +420,8 @@ __device__ __forceinline__ void relax(const CellArgs& A, const K& k, int nb, int
     const int lu = q.head - k.x0;
     const long long pu = prc()[lu];
     int* D = dst(k);
-    long long len = PR ? pu - q.cost - pv + 1 : floordiv(pu - q.cost - pv, k.eps) + 1;
+    const long long x = pu - q.cost - pv;
+    long long len = PR ? x + 1 : (k.eps_shift >= 0 ? (x >> k.eps_shift) : floordiv(x, k.eps)) + 1;
     if (!PR) len = len < 0 ? 0 : (len > DCAP ? DCAP : len);
     else len = len > DCAP ? DCAP : (len < DNEG ? DNEG : len);
     long long cand = (long long)dv + len;
@@ -418,10 +451,8 @@ __device__ __forceinline__ void bf_grp(const CellArgs& A, K& k, int nb, int v) {
     const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
-        if (a < en) {
-            relax<PR>(A, k, nb, a, dv, pv);
-            k.guscans++;
-        }
+        if (a < en) relax<PR>(A, k, nb, a, dv, pv);
+        wcount(C_GUSCAN, a < en);
     }
 }
 
@@ -432,9 +463,10 @@ __device__ __forceinline__ void bf_hub(const CellArgs& A, K& k, int nb, int v) {
     if (!PR && dv >= DINF) return;
     int b0, en;
     seg(A, v, b0, en);
-    for (int a = b0 + (int)threadIdx.x; a < en; a += CT) {
-        relax<PR>(A, k, nb, a, dv, pv);
-        k.guscans++;
+    for (int base = b0; base < en; base += CT) {   // (a uniform trip count: the ballot needs the whole wave)
+        const int a = base + (int)threadIdx.x;
+        if (a < en) relax<PR>(A, k, nb, a, dv, pv);
+        wcount(C_GUSCAN, a < en);
     }
 }
 
@@ -455,6 +487,7 @@ __device__ __forceinline__ void sat_grp(const CellArgs& A, K& k, int v, long lon
     long long tot = 0;
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
+        bool pushed = false;
         if (a < en) {
             const Pos q = ld_pos(A.pos + a);
             if (q.rcap > 0 && q.cost + pv - P[q.head - k.x0] < -thr) {
@@ -462,9 +495,10 @@ __device__ __forceinline__ void sat_grp(const CellArgs& A, K& k, int v, long lon
                 A.pos[q.rev].rcap = q.ucap;
                 add_ex(A, q.head, q.rcap);
                 tot += q.rcap;
-                k.pushes++;
+                pushed = true;
             }
         }
+        wcount(C_PUSH, pushed);
     }
     tot = g_sum<G>(tot);
     if (v >= 0 && lig == 0 && tot) add_ex(A, v, -tot);
@@ -476,44 +510,155 @@ __device__ __forceinline__ void sat_hub(const CellArgs& A, K& k, int v, long lon
     int b0, en;
     seg(A, v, b0, en);
     long long tot = 0;
-    for (int a = b0 + (int)threadIdx.x; a < en; a += CT) {
-        const Pos q = ld_pos(A.pos + a);
-        if (q.rcap > 0 && q.cost + pv - P[q.head - k.x0] < -thr) {
-            A.pos[a].rcap = 0;
-            A.pos[q.rev].rcap = q.ucap;
-            add_ex(A, q.head, q.rcap);
-            tot += q.rcap;
-            k.pushes++;
+    for (int base = b0; base < en; base += CT) {
+        const int a = base + (int)threadIdx.x;
+        bool pushed = false;
+        if (a < en) {
+            const Pos q = ld_pos(A.pos + a);
+            if (q.rcap > 0 && q.cost + pv - P[q.head - k.x0] < -thr) {
+                A.pos[a].rcap = 0;
+                A.pos[q.rev].rcap = q.ucap;
+                add_ex(A, q.head, q.rcap);
+                tot += q.rcap;
+                pushed = true;
+            }
         }
+        wcount(C_PUSH, pushed);
     }
     tot = blk_sum(tot);
     if (threadIdx.x == 0 && tot) add_ex(A, v, -tot);
 }
 
-// ------------------------------------------------------------------ step ---
-template <int OP, int C>
-__device__ __forceinline__ void item(const CellArgs& A, K& k, int src, int nb, int j, int n, long long thr) {
-    constexpr int G = C < 5 ? (4 << C) : 64;
-    constexpr int PER = 64 / G;
-    int v = -1;
-    if (C < 5) {
-        const int idx = j * PER + lane() / G;
-        if (idx < n) v = node_at(A, src, C, idx);
-    } else {
-        v = __builtin_amdgcn_readfirstlane(node_at(A, src, C, j));
+// ------------------------------------------------ one thread per node ---
+// Classes of ≤ 32 positions (tasks, PUs, machines): a node per thread, its
+// positions loaded CH at a time (independent loads in flight), the excess spread
+// along them in order — the same distribution as the lane-group prefix sum, with
+// no cross-lane exchange, and 64 nodes per wave instead of 64/G.
+constexpr int CH = 4;
+
+__device__ __forceinline__ void sweep_thr(const CellArgs& A, K& k, int nb, int v, Tc& t) {
+    const long long* P = prc();
+    long long e = 0, pv = 0;
+    int b0 = 0, en = 0;
+    if (v >= 0) {
+        e = ld_ex(A, v);
+        pv = P[v - k.x0];
+        seg(A, v, b0, en);
     }
-    if (OP == OP_SWEEP) sweep_grp<G>(A, k, nb, v);
-    else if (OP == OP_BF) bf_grp<G, false>(A, k, nb, v);
-    else if (OP == OP_PR) bf_grp<G, true>(A, k, nb, v);
-    else sat_grp<G>(A, k, v, thr);
+    if (e <= 0) return;
+    ++t.c[C_VISIT];
+    long long rem = e, minc = INF64;
+    for (int a0 = b0; a0 < en; a0 += CH) {
+        Pos q[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (a0 + u < en) q[u] = ld_pos(A.pos + a0 + u);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            if (a0 + u >= en) break;
+            ++t.c[C_SCAN];
+            const long long r = q[u].rcap;
+            const long long cr = q[u].cost + pv - P[q[u].head - k.x0];
+            long long d = 0;
+            if (cr < 0 && r > 0) {
+                d = rem < r ? rem : r;
+                if (d > 0) {
+                    push(A, k, nb, a0 + u, q[u].head, r, d, q[u].rev, q[u].ucap);
+                    ++t.c[C_PUSH];
+                    rem -= d;
+                }
+                if (r - d > 0) minc = min(minc, cr);
+            } else if (r > 0 || cr <= k.eps) {
+                minc = min(minc, cr);
+            }
+        }
+        if (rem == 0) break;
+    }
+    const long long pushed = e - rem;
+    if (pushed) add_ex(A, v, -pushed);
+    if (rem > 0) {
+        if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
+        else relabel(A, k, v, pv - (minc + k.eps));
+        ++t.c[C_RELABEL];
+        mark(A, k, nb, v);
+    }
+}
+
+template <bool PR>
+__device__ __forceinline__ void bf_thr(const CellArgs& A, K& k, int nb, int v, Tc& t) {
+    int dv = DINF;
+    long long pv = 0;
+    int b0 = 0, en = 0;
+    if (v >= 0) {
+        dv = dst(k)[v - k.x0];
+        pv = prc()[v - k.x0];
+        seg(A, v, b0, en);
+    }
+    if (!PR && dv >= DINF) return;
+    for (int a0 = b0; a0 < en; a0 += CH) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (a0 + u < en) {
+                relax<PR>(A, k, nb, a0 + u, dv, pv);
+                ++t.c[C_GUSCAN];
+            }
+    }
+}
+
+__device__ __forceinline__ void sat_thr(const CellArgs& A, K& k, int v, long long thr, Tc& t) {
+    const long long* P = prc();
+    long long pv = 0;
+    int b0 = 0, en = 0;
+    if (v >= 0) {
+        pv = P[v - k.x0];
+        seg(A, v, b0, en);
+    }
+    long long tot = 0;
+    for (int a0 = b0; a0 < en; a0 += CH) {
+        Pos q[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (a0 + u < en) q[u] = ld_pos(A.pos + a0 + u);
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (a0 + u < en && q[u].rcap > 0 && q[u].cost + pv - P[q[u].head - k.x0] < -thr) {
+                A.pos[a0 + u].rcap = 0;
+                A.pos[q[u].rev].rcap = q[u].ucap;
+                add_ex(A, q[u].head, q[u].rcap);
+                tot += q[u].rcap;
+                ++t.c[C_PUSH];
+            }
+    }
+    if (tot) add_ex(A, v, -tot);
+}
+
+// ------------------------------------------------------------------ step ---
+// An item: 64 nodes of a class ≤ 32 positions (one per thread), or one node of
+// the ≤ 64 / ≤ 512-position classes (the wave).
+template <int OP, int C>
+__device__ __forceinline__ void item(const CellArgs& A, K& k, int src, int nb, int j, int n, long long thr, Tc& t) {
+    if (C < 4) {
+        const int idx = j * 64 + lane();
+        const int v = idx < n ? node_at(A, src, C, idx) : -1;
+        if (OP == OP_SWEEP) sweep_thr(A, k, nb, v, t);
+        else if (OP == OP_BF) bf_thr<false>(A, k, nb, v, t);
+        else if (OP == OP_PR) bf_thr<true>(A, k, nb, v, t);
+        else sat_thr(A, k, v, thr, t);
+        return;
+    }
+    const int v = __builtin_amdgcn_readfirstlane(node_at(A, src, C, j));
+    if (OP == OP_SWEEP) sweep_grp<64>(A, k, nb, v);
+    else if (OP == OP_BF) bf_grp<64, false>(A, k, nb, v);
+    else if (OP == OP_PR) bf_grp<64, true>(A, k, nb, v);
+    else sat_grp<64>(A, k, v, thr);
 }
 
 // One step over frontier src (2: every node) into buffer nb: the workgroup-
 // sized nodes one after another with every thread, then the rest as items
 // (a batch of 64/G nodes of one class, or one ≤ 512-position node) dealt to the
-// 16 waves. Ends with buffer nb complete and src emptied, behind a barrier.
+// 16 waves. The caller's barrier completes buffer nb; step_post then empties src.
 template <int OP>
-__device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, long long thr, unsigned long long t0) {
+__device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, long long thr) {
     const int n6 = count_of(src, 6);
     for (int j = 0; j < n6; ++j) {
         const int v = node_at(A, src, 6, j);
@@ -525,21 +670,29 @@ __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, l
     }
     const int n0 = count_of(src, 0), n1 = count_of(src, 1), n2 = count_of(src, 2), n3 = count_of(src, 3),
               n4 = count_of(src, 4), n5 = count_of(src, 5);
-    const int e0 = (n0 + 15) >> 4;
-    const int e1 = e0 + ((n1 + 7) >> 3);
-    const int e2 = e1 + ((n2 + 3) >> 2);
-    const int e3 = e2 + ((n3 + 1) >> 1);
+    const int e0 = (n0 + 63) >> 6;
+    const int e1 = e0 + ((n1 + 63) >> 6);
+    const int e2 = e1 + ((n2 + 63) >> 6);
+    const int e3 = e2 + ((n3 + 63) >> 6);
     const int e4 = e3 + n4;
     const int e5 = e4 + n5;
+    Tc t;
     for (int it = wid(); it < e5; it += NW) {
-        if (it < e0) item<OP, 0>(A, k, src, nb, it, n0, thr);
-        else if (it < e1) item<OP, 1>(A, k, src, nb, it - e0, n1, thr);
-        else if (it < e2) item<OP, 2>(A, k, src, nb, it - e1, n2, thr);
-        else if (it < e3) item<OP, 3>(A, k, src, nb, it - e2, n3, thr);
-        else if (it < e4) item<OP, 4>(A, k, src, nb, it - e3, n4, thr);
-        else item<OP, 5>(A, k, src, nb, it - e4, n5, thr);
+        if (it < e0) item<OP, 0>(A, k, src, nb, it, n0, thr, t);
+        else if (it < e1) item<OP, 1>(A, k, src, nb, it - e0, n1, thr, t);
+        else if (it < e2) item<OP, 2>(A, k, src, nb, it - e1, n2, thr, t);
+        else if (it < e3) item<OP, 3>(A, k, src, nb, it - e2, n3, thr, t);
+        else if (it < e4) item<OP, 4>(A, k, src, nb, it - e3, n4, thr, t);
+        else item<OP, 5>(A, k, src, nb, it - e4, n5, thr, t);
     }
-    __syncthreads();
+    flush(t);
+}
+
+// After a step's barrier: src emptied; a sweep's relabels take effect; the
+// pending-relabel counter of the NEXT sweep's parity is reset (it was last read
+// before the previous barrier).
+template <int OP>
+__device__ __forceinline__ void step_post(const CellArgs& A, const K& k, int src) {
     if (src < 2) {
         if (threadIdx.x < 8) s_.cnt[src][threadIdx.x] = 0;
         unsigned* bm = bmp(k);
@@ -549,10 +702,8 @@ __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, l
         long long* P = prc();
         const int nr = s_.rl_cnt[k.sp];
         for (int i = threadIdx.x; i < nr; i += CT) P[A.rl_node[k.x0 + i] - k.x0] = A.rl_p[k.x0 + i];
-        if (threadIdx.x == 0) s_.rl_cnt[k.sp ^ 1] = 0;   // the next sweep's buffer (read before the last barrier)
+        if (threadIdx.x == 0) s_.rl_cnt[k.sp ^ 1] = 0;
     }
-    if (threadIdx.x == 0 && __builtin_amdgcn_s_memrealtime() - t0 > A.timeout_ticks) s_.stop = 1;
-    __syncthreads();
 }
 
 // ---------------------------------------------------------- control ---
@@ -574,7 +725,9 @@ struct Ctl {
     int peak, cyc_sweeps, upd_rounds, pr_rounds, pr_cap, pr_ok_now, pr_next, nexc;
     int updates, pr_ok, pr_tries, ended_at_one;
     unsigned long long phase_sweeps, sweeps, rounds;
-    unsigned long long scans, visits, pushes, relabels, guscans;
+    unsigned long long t_op;                // when the running operation started
+    unsigned long long op_ticks[O_DONE];    // 100 MHz ticks per operation kind (incl. its barriers)
+    unsigned op_n[O_DONE];
 };
 __shared__ Ctl c_;
 
@@ -617,9 +770,13 @@ __device__ __forceinline__ void phase_end(const CellArgs& A) {
     }
 }
 
-__device__ void control(const CellArgs& A, int N) {
+__device__ __forceinline__ void control(const CellArgs& A, int N) {
     Ctl& c = c_;
-    if (s_.stop) return finish(CS_TIMEOUT);
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    c.op_ticks[c.op] += now - c.t_op;
+    ++c.op_n[c.op];
+    c.t_op = now;
+    if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
     switch (c.op) {
         case O_SAT:
             c.op = O_GUINIT;
@@ -763,23 +920,11 @@ __device__ __forceinline__ void gu_fin(const CellArgs& A, const K& k) {
     if (threadIdx.x == 0) c_.nexc = n;
 }
 
-__device__ __forceinline__ void flush_counts(const K& k) {
-    const long long sc = g_sum<64>((long long)k.scans), vi = g_sum<64>((long long)k.visits),
-                    pu = g_sum<64>((long long)k.pushes), rl = g_sum<64>((long long)k.relabels),
-                    gs = g_sum<64>((long long)k.guscans);
-    if (lane() == 0 && (sc | vi | pu | rl | gs)) {
-        if (sc) atomicAdd(&c_.scans, (unsigned long long)sc);
-        if (vi) atomicAdd(&c_.visits, (unsigned long long)vi);
-        if (pu) atomicAdd(&c_.pushes, (unsigned long long)pu);
-        if (rl) atomicAdd(&c_.relabels, (unsigned long long)rl);
-        if (gs) atomicAdd(&c_.guscans, (unsigned long long)gs);
-    }
-}
-
 __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
     const CellDesc cd = A.cells[blockIdx.x];
     const int N = cd.cb[CELL_NCLS] - cd.cb[0];
     if (threadIdx.x < 8) s_.cbs[threadIdx.x] = A.cells[blockIdx.x].cb[threadIdx.x];
+    if (threadIdx.x < NCTR) ctr_[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         s_.rl_cnt[0] = s_.rl_cnt[1] = 0;
         s_.flag = 0;
@@ -787,6 +932,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         Ctl& c = c_;
         c = Ctl{};
         c.t0 = __builtin_amdgcn_s_memrealtime();
+        c.t_op = c.t0;
         c.eps_ph = A.eps_start;
         c.eps = 1;
         if (N == 0) {
@@ -817,6 +963,8 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         }
     }
     __syncthreads();
+    // one operation per iteration: its body, a barrier, the post-work of steps
+    // with the controller's decision (thread 0), a barrier
     for (;;) {
         const int op = c_.op;
         if (op == O_DONE) break;
@@ -832,13 +980,12 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         k.c5 = cd.cb[5];
         k.c6 = cd.cb[6];
         k.eps = c_.eps;
+        k.eps_shift = (k.eps & (k.eps - 1)) == 0 ? __builtin_ctzll((unsigned long long)k.eps) : -1;
         k.sp = c_.sp;
-        k.scans = k.visits = k.pushes = k.relabels = k.guscans = 0;
         const int src = c_.src, nb = c_.nb;
-        const unsigned long long t0 = c_.t0;
         switch (op) {
             case O_SAT:
-                step<OP_SAT>(A, k, 2, 0, c_.thr, t0);
+                step<OP_SAT>(A, k, 2, 0, c_.thr);
                 break;
             case O_GUINIT:
                 reset_lists(k);
@@ -846,7 +993,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
                 gu_init(A, k);
                 break;
             case O_BF:
-                step<OP_BF>(A, k, src, nb, 0, t0);
+                step<OP_BF>(A, k, src, nb, 0);
                 break;
             case O_GUFIN:
                 reset_lists(k);
@@ -854,7 +1001,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
                 gu_fin(A, k);
                 break;
             case O_SWEEP:
-                step<OP_SWEEP>(A, k, src, nb, 0, t0);
+                step<OP_SWEEP>(A, k, src, nb, 0);
                 break;
             case O_PRINIT: {
                 int* D = dst(k);
@@ -864,7 +1011,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
                 break;
             }
             case O_PR:
-                step<OP_PR>(A, k, src, nb, 0, t0);
+                step<OP_PR>(A, k, src, nb, 0);
                 break;
             case O_PRFIN:
                 if (c_.pr_ok_now) {
@@ -877,8 +1024,10 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
             default:
                 break;
         }
-        flush_counts(k);
         __syncthreads();
+        if (op == O_BF) step_post<OP_BF>(A, k, src);
+        else if (op == O_SWEEP) step_post<OP_SWEEP>(A, k, src);
+        else if (op == O_PR) step_post<OP_PR>(A, k, src);
         if (threadIdx.x == 0) control(A, N);
         __syncthreads();
     }
@@ -902,12 +1051,16 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         o.last_eps = c.ended_at_one;
         o.sweeps = c.sweeps;
         o.bf_rounds = c.rounds;
-        o.scans = c.scans;
-        o.visits = c.visits;
-        o.pushes = c.pushes;
-        o.relabels = c.relabels;
-        o.gu_scans = c.guscans;
+        o.scans = ctr_[C_SCAN];
+        o.visits = ctr_[C_VISIT];
+        o.pushes = ctr_[C_PUSH];
+        o.relabels = ctr_[C_RELABEL];
+        o.gu_scans = ctr_[C_GUSCAN];
         o.ticks = __builtin_amdgcn_s_memrealtime() - c.t0;
+        for (int i = 0; i < CELL_NOPS; ++i) {
+            o.op_ticks[i] = c.op_ticks[i];
+            o.op_n[i] = c.op_n[i];
+        }
         A.out[blockIdx.x] = o;
     }
 }

@@ -4071,6 +4071,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         const long long D = o.final_div < 0 ? 0 : (o.final_div > 0 ? o.final_div : 48);
         if (D > 0 && use_pr && maxc > 0) {
             long long e = std::max<long long>(1, (mult - 1) / D);
+            // the cell solver's ladder is powers of two (α = 8): its arc lengths
+            // floor(rc/ε) are then shifts (the final phase lands in (1/2D, 1/D] of a unit)
+            if (s.cell_layout && (alpha & (alpha - 1)) == 0)
+                while (e & (e - 1)) e &= e - 1;
             const long long lo = std::max<long long>(1, eps / ((long long)alpha * alpha));
             while (e < lo && e <= (1LL << 58) / alpha) e *= alpha;
             eps = e * alpha;   // the loop divides before each phase
@@ -4346,7 +4350,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         KS_CHECK(read_ctl());
         const long long viol = s.h_ctl->gu_L;
-        const long long e0 = std::max<long long>(1, std::min<long long>({viol, 8 * mult, eps}));
+        long long e0 = std::max<long long>(1, std::min<long long>({viol, 8 * mult, eps}));
+        if (s.cell_layout && (alpha & (alpha - 1)) == 0)   // a power of two ≥ the violation (cell ladder)
+            while (e0 & (e0 - 1)) e0 += e0 & -e0;
         warm_thr = e0;
         eps = e0 * alpha;   // the first phase runs at e0
         KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
@@ -4407,6 +4413,19 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             cticks_sum += o.ticks;
         }
         phases += pmax;
+        if (cycle_log) {   // per-operation device time of the slowest cell (ks_opts.log_cycles)
+            size_t w = 0;
+            for (size_t i = 1; i < s.h_cell_out.size(); ++i)
+                if (s.h_cell_out[i].ticks > s.h_cell_out[w].ticks) w = i;
+            const CellOut& o = s.h_cell_out[w];
+            static const char* names[CELL_NOPS] = {"sat", "gu_init", "bf", "gu_fin", "sweep", "pr_init", "pr", "pr_fin"};
+            std::fprintf(stderr, "cell %zu of %d: %.3f ms, phases %d updates %d sweeps %llu rounds %llu:", w, ncells,
+                         o.ticks / 1e5, o.phases, o.updates, o.sweeps, o.bf_rounds);
+            for (int i = 0; i < CELL_NOPS; ++i)
+                if (o.op_n[i])
+                    std::fprintf(stderr, " %s %u x %.2f us", names[i], o.op_n[i], o.op_ticks[i] / 100.0 / o.op_n[i]);
+            std::fprintf(stderr, "\n");
+        }
         return worst;
     };
     auto cell_status = [&](int cs, const char* what) -> int {
