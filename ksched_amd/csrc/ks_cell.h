@@ -39,7 +39,26 @@ struct CellDesc {
     int cb[CELL_NCLS + 1];
 };
 
-enum CellStatus { CS_OK = 0, CS_INFEASIBLE = 1, CS_NOCONV = 2, CS_TIMEOUT = 3 };
+// The cell solver's 16-byte copy of a residual position (packed before a solve
+// from the 32-byte ks_pos.h record, its residual written back after): residual and
+// pair capacity (int32), the UNSCALED cost (int32; CELL_DEAD for an inert
+// position), the head as a cell-local node index (14 bits) and the reverse
+// position relative to the cell's first position (18 bits). A task's eight
+// positions are one 128-byte line instead of two.
+struct alignas(16) CellPos {
+    int rcap;
+    int ucap;
+    int cost;
+    unsigned hr;             // head_local | rev_rel << CELL_HEAD_BITS
+};
+constexpr int CELL_HEAD_BITS = 14;
+constexpr int CELL_MAX_POS = 1 << (32 - CELL_HEAD_BITS);   // positions per cell the record addresses
+constexpr int CELL_DEAD = 0x7fffffff;                       // an inert position's cost
+constexpr long long CELL_MAX_CAP = (1LL << 24) - 1;         // capacities the cell solver takes (a lane group's
+                                                            // admissible sum then fits int32) and |cost|
+constexpr long long CELL_MAX_COST = (1LL << 30) - 1;
+
+enum CellStatus { CS_OK = 0, CS_INFEASIBLE = 1, CS_NOCONV = 2, CS_TIMEOUT = 3, CS_RANGE = 4 };
 
 // Written by the cell's workgroup when it finishes.
 struct CellOut {
@@ -57,11 +76,18 @@ struct CellOut {
     // barriers and the controller, and counts
     unsigned long long op_ticks[8];
     unsigned op_n[8];
+    unsigned long long item_ticks[8];    // diagnostics: op start → the last wave's items done
+    unsigned long long first_ticks[8];   //              op start → the first wave's items done
+    unsigned long long cls_ticks[32];    //              item ticks by step (sweep, BF, refinement, saturate) × class
+    unsigned cls_n[32];                  //              and items (class 6: the workgroup-sized nodes)
 };
 constexpr int CELL_NOPS = 8;
 
 struct CellArgs {
     Pos* pos;
+    CellPos* cp;             // m2 compact positions (k_cell_pack before, k_cell_unpack after)
+    const int* first;        // segment starts (a cell's positions begin at first[cb[0]])
+    int m2;
     long long* nd;           // node records (p0, dist, p1, packed segment) × nn
     long long* excess;
     const CellDesc* cells;
@@ -84,12 +110,15 @@ struct CellArgs {
     int mode;                // 0: solve from the state in place; 1: certificate recovery at ε = 1
     int max_nodes;           // largest cell (sizes the LDS)
     unsigned long long timeout_ticks;   // a cell's solve gives up after this many 100 MHz ticks
+    const int* bad;          // set by k_cell_pack: a value the compact record cannot hold
 };
 
 // LDS one workgroup needs for cells of up to n nodes (0 when they do not fit).
 size_t cell_lds_bytes(int n);
-// Largest cell the LDS holds.
+// Largest cell the LDS holds (and the compact record's head field addresses).
 int cell_max_nodes();
-hipError_t cell_launch(const CellArgs& a, hipStream_t st);
+// k_cell_pack → k_cell → k_cell_unpack on st; *bad (device int) is set when a
+// position does not fit the compact record (every cell then returns CS_RANGE).
+hipError_t cell_launch(const CellArgs& a, int* bad, hipStream_t st);
 
 }  // namespace ks

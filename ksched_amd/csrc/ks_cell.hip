@@ -32,6 +32,8 @@
 // read by one thread and broadcast through LDS), so a workgroup always exits.
 #include "ks_cell.h"
 
+#include <algorithm>
+
 namespace ks {
 namespace {
 
@@ -52,6 +54,7 @@ struct St {
     int rl_cnt[2];        // pending relabels, by sweep parity
     int flag;             // F_INFEAS | F_NEG
     int stop;             // the wall-clock limit was hit
+    int next;             // the step's next item (waves take items dynamically)
     long long red[NW];
 };
 
@@ -66,24 +69,22 @@ extern __shared__ long long dyn_[];
 // the kernel argument itself (A), which keeps them global-address-space loads.
 struct K {
     int x0, N, W, maxn;
+    int pb;               // the cell's first position (compact records address reverses from it)
     int c1, c2, c3, c4, c5, c6;
     long long eps;
     int eps_shift;        // log2 ε when ε is a power of two (the cell ladder's are), else −1
     int sp;               // sweep parity (pending-relabel buffer)
 };
 
-// Work counters (ks_result units), counted per wave where the work happens: one
-// ballot and, when any lane did work, one LDS add by lane 0 (the ballot must be
-// taken at a point where the whole wave is converged).
+// Work counters (ks_result units): counted per lane in registers, summed over the
+// wave by DPP (no LDS round trips) and added to the workgroup's counters once per
+// step.
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, NCTR = 5 };
 __shared__ unsigned long long ctr_[NCTR];
+__shared__ unsigned long long t_items_, t_first_;   // diagnostics: last / first wave's items done
+__shared__ unsigned long long cls_t_[4][8];          // diagnostics: item ticks by step kind × node class
+__shared__ unsigned cls_n_[4][8];                    //              and items
 __device__ __forceinline__ int lane();
-__device__ __forceinline__ void wcount(int i, bool pred) {
-    const unsigned long long m = __ballot(pred);
-    if (m && lane() == 0) atomicAdd(&ctr_[i], (unsigned long long)__popcll(m));
-}
-// Thread-per-node work counts per thread, summed over the wave by DPP (no LDS
-// round trips) and added to the workgroup's counters once per step.
 struct Tc {
     unsigned c[NCTR] = {0, 0, 0, 0, 0};
 };
@@ -142,6 +143,22 @@ __device__ __forceinline__ Pos ld_pos(const Pos* p) {
     r.rev = (int)(unsigned)((unsigned long long)b.y >> 32);
     return r;
 }
+// A compact position (ks_cell.h CellPos) decoded into the engine's field names:
+// scaled cost, residual, pair capacity, absolute head and reverse position.
+constexpr long long DEAD_SCALED = 1LL << 60;
+__device__ __forceinline__ int4 ld_raw(const CellArgs& A, int a) { return *reinterpret_cast<const int4*>(A.cp + a); }
+__device__ __forceinline__ Pos dec(const CellArgs& A, const K& k, int4 w) {
+    Pos r;
+    r.rcap = w.x;
+    r.ucap = w.y;
+    r.cost = w.z == CELL_DEAD ? DEAD_SCALED : (long long)w.z * A.mult;
+    r.head = k.x0 + (int)((unsigned)w.w & ((1u << CELL_HEAD_BITS) - 1));
+    r.rev = k.pb + (int)((unsigned)w.w >> CELL_HEAD_BITS);
+    return r;
+}
+__device__ __forceinline__ Pos ld_cp(const CellArgs& A, const K& k, int a) { return dec(A, k, ld_raw(A, a)); }
+__device__ __forceinline__ void st_rcap(const CellArgs& A, int a, long long v) { A.cp[a].rcap = (int)v; }
+
 __device__ __forceinline__ void seg(const CellArgs& A, int x, int& b0, int& b1) {
     const unsigned long long w = (unsigned long long)A.nd[ni(x) + 3];
     b0 = (int)(unsigned)(w & 0xffffffffULL);
@@ -172,10 +189,6 @@ __device__ __forceinline__ long long g_incl_scan(long long x) {
     return x;
 }
 template <int G>
-__device__ __forceinline__ long long g_last(long long x) {   // the group's last lane's value
-    return bperm64(lane() | (G - 1), x);
-}
-template <int G>
 __device__ __forceinline__ long long g_min(long long x) {
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) x = min(x, bperm64(lane() ^ o, x));
@@ -191,6 +204,62 @@ template <int G>
 __device__ __forceinline__ long long g_max(long long x) {
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) x = max(x, bperm64(lane() ^ o, x));
+    return x;
+}
+
+// DPP lane-group scans (G = 4…64, aligned groups): row_shr within 16-lane rows,
+// then row_bcast:15 / :31 across rows. The inclusive result of the group's LAST
+// lane is the group total (sum) or minimum (min): leaf groups lead from that lane,
+// so no broadcast is needed.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
+}
+// l = lane & (G − 1), computed once by the caller: lane() is a volatile asm, a
+// scheduling barrier that would keep a batch's loads apart.
+template <int G>
+__device__ __forceinline__ int gs_add(int x, int l) {
+    int y = dpp_i32<0x111, 0xf>(x);   // row_shr:1
+    if (l >= 1) x += y;
+    y = dpp_i32<0x112, 0xf>(x);       // row_shr:2
+    if (l >= 2) x += y;
+    if (G > 4) {
+        y = dpp_i32<0x114, 0xf>(x);   // row_shr:4
+        if (l >= 4) x += y;
+    }
+    if (G > 8) {
+        y = dpp_i32<0x118, 0xf>(x);   // row_shr:8
+        if (l >= 8) x += y;
+    }
+    if (G > 16) x += dpp_i32<0x142, 0xa>(x);   // row_bcast:15 → rows 1, 3
+    if (G > 32) x += dpp_i32<0x143, 0xc>(x);   // row_bcast:31 → rows 2, 3
+    return x;
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ long long dpp_i64(long long v, long long fill) {
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned long long)fill, (int)(unsigned long long)v, CTRL,
+                                               ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)((unsigned long long)fill >> 32),
+                                               (int)((unsigned long long)v >> 32), CTRL, ROW_MASK, 0xf, false);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// inclusive prefix minimum over the group (64-bit); the last lane holds the group min
+template <int G>
+__device__ __forceinline__ long long gs_min(long long x, int l) {
+    long long y = dpp_i64<0x111, 0xf>(x, INF64);
+    if (l >= 1) x = min(x, y);
+    y = dpp_i64<0x112, 0xf>(x, INF64);
+    if (l >= 2) x = min(x, y);
+    if (G > 4) {
+        y = dpp_i64<0x114, 0xf>(x, INF64);
+        if (l >= 4) x = min(x, y);
+    }
+    if (G > 8) {
+        y = dpp_i64<0x118, 0xf>(x, INF64);
+        if (l >= 8) x = min(x, y);
+    }
+    if (G > 16) x = min(x, dpp_i64<0x142, 0xa>(x, INF64));
+    if (G > 32) x = min(x, dpp_i64<0x143, 0xc>(x, INF64));
     return x;
 }
 
@@ -278,8 +347,8 @@ __device__ __forceinline__ void reset_lists(const K& k) {
 // ------------------------------------------------------------ push/relabel ---
 __device__ __forceinline__ void push(const CellArgs& A, const K& k, int nb, int a, int w, long long r, long long d,
                                      int rv, long long uc) {
-    A.pos[a].rcap = r - d;
-    A.pos[rv].rcap = uc - (r - d);
+    st_rcap(A, a, r - d);
+    st_rcap(A, rv, uc - (r - d));
     add_ex(A, w, d);
     mark(A, k, nb, w);
 }
@@ -290,63 +359,88 @@ __device__ __forceinline__ void relabel(const CellArgs& A, const K& k, int v, lo
     A.rl_p[k.x0 + i] = np;
 }
 
-// One node per G-lane group (G = 64 loops over 64-position chunks): the excess
-// is spread over the admissible arcs by an in-group prefix sum; a node that
-// saturates all of them relabels to p − (minc + ε), minc over residual arcs and
-// over arcs of reduced cost in (0, ε] (ks_engine.hip sweep_group).
-template <int G>
-__device__ __forceinline__ void sweep_grp(const CellArgs& A, K& k, int nb, int v) {
+// Wave- and workgroup-sized nodes walk their positions UC chunks at a time: every
+// chunk's record loads are issued before the first is used (one chunk per round
+// trip left a 450-position aggregator eight dependent L2 latencies per visit).
+constexpr int UC = 4;
+
+__device__ __forceinline__ long long uni64(long long x) {   // a wave-uniform copy (x is the same in every lane)
+    const unsigned long long u = (unsigned long long)x;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ long long lane63_64(long long x) {
+    const unsigned long long u = (unsigned long long)x;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// The relabel minimum over v's positions: residual arcs (admissible ones only when
+// the push left residual) and arcs of reduced cost in (0, ε] (ks_engine.hip
+// sweep_group).
+__device__ __forceinline__ void minc_acc(long long& minc, bool valid, long long cr, int r, int d, long long eps) {
+    if (!valid) return;
+    if (cr < 0) {
+        if (r - d > 0) minc = min(minc, cr);
+    } else if (r > 0 || cr <= eps) {
+        minc = min(minc, cr);
+    }
+}
+
+// One node per wave (classes of ≤ 64 and ≤ 512 positions; v uniform): the excess
+// is spread over the admissible arcs in position order by a wave prefix sum; a
+// node that saturates all of them relabels to p − (minc + ε).
+__device__ __forceinline__ void sweep_wave(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const long long* P = prc();
-    const int lig = lane() & (G - 1);
-    long long e = 0, pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        e = ld_ex(A, v);
-        pv = P[v - k.x0];
-        seg(A, v, b0, en);
-    }
-    const bool act = e > 0;
-    if (!act) en = b0;
-    wcount(C_VISIT, act && lig == 0);
+    const long long e = uni64(ld_ex(A, v));
+    if (e <= 0) return;
+    const long long pv = P[v - k.x0];
+    int b0, en;
+    seg(A, v, b0, en);
+    const int ln = lane();
+    t.c[C_VISIT] += ln == 0;
     long long rem = e, minc = INF64;
-    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
-    for (int it = 0; it < iters; ++it) {
-        const int a = b0 + it * G + lig;
-        const bool valid = a < en;
-        long long r = 0, cr = 0, uc = 0;
-        int w = 0, rv = 0;
-        if (valid) {
-            const Pos q = ld_pos(A.pos + a);
-            r = q.rcap;
-            w = q.head;
-            rv = q.rev;
-            uc = q.ucap;
-            cr = q.cost + pv - P[w - k.x0];
+    for (int base = b0; base < en; base += 64 * UC) {
+        int4 qr[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int a = base + 64 * u + ln;
+            qr[u] = ld_raw(A, a < en ? a : b0);
         }
-        wcount(C_SCAN, valid);
-        const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
-        const long long incl = g_incl_scan<G>(adm);
-        const long long total = g_last<G>(incl);
-        long long d = rem - (incl - adm);
-        d = d < 0 ? 0 : (d > adm ? adm : d);
-        if (d > 0) push(A, k, nb, a, w, r, d, rv, uc);
-        wcount(C_PUSH, d > 0);
-        if (valid) {
-            if (cr < 0) {
-                if (r - d > 0) minc = min(minc, cr);
-            } else if (r > 0 || cr <= k.eps) {
-                minc = min(minc, cr);
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const Pos Q = dec(A, k, qr[u]);
+            const int a = base + 64 * u + ln;
+            const bool valid = a < en;
+            int r = 0;
+            long long cr = 0;
+            if (valid) {
+                r = (int)Q.rcap;
+                cr = Q.cost + pv - P[Q.head - k.x0];
             }
+            t.c[C_SCAN] += valid;
+            const int adm = (valid && cr < 0 && r > 0) ? r : 0;
+            const int incl = gs_add<64>(adm, ln);
+            const int tot = __builtin_amdgcn_readlane(incl, 63);
+            const long long ex = rem - (incl - adm);
+            const int d = ex <= 0 ? 0 : (ex < adm ? (int)ex : adm);
+            if (d > 0) {
+                push(A, k, nb, a, Q.head, r, d, Q.rev, Q.ucap);
+                ++t.c[C_PUSH];
+            }
+            minc_acc(minc, valid, cr, r, d, k.eps);
+            rem -= tot < rem ? tot : rem;
         }
-        rem -= total < rem ? total : rem;
-        if (G == 64 && rem == 0) break;
+        if (rem == 0) break;
     }
-    minc = g_min<G>(minc);
-    wcount(C_RELABEL, act && lig == 0 && rem > 0);
-    if (act && lig == 0) {
+    minc = lane63_64(gs_min<64>(minc, ln));
+    if (ln == 63) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
         if (rem > 0) {
+            ++t.c[C_RELABEL];
             if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
             else relabel(A, k, v, pv - (minc + k.eps));
             mark(A, k, nb, v);
@@ -355,53 +449,55 @@ __device__ __forceinline__ void sweep_grp(const CellArgs& A, K& k, int nb, int v
 }
 
 // The same for a node above 512 positions: the whole workgroup, 1024 positions
-// per pass, the excess spread by a workgroup-wide prefix sum. v is uniform.
-__device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v) {
+// per chunk, the excess spread by a workgroup-wide prefix sum. v is uniform.
+__device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const long long* P = prc();
     const long long e = ld_ex(A, v);
     const long long pv = P[v - k.x0];
     int b0, en;
     seg(A, v, b0, en);
     if (e <= 0) return;
-    wcount(C_VISIT, threadIdx.x == 0);
+    t.c[C_VISIT] += threadIdx.x == 0;
     long long rem = e, minc = INF64;
-    for (int base = b0; base < en; base += CT) {
-        const int a = base + (int)threadIdx.x;
-        const bool valid = a < en;
-        long long r = 0, cr = 0, uc = 0;
-        int w = 0, rv = 0;
-        if (valid) {
-            const Pos q = ld_pos(A.pos + a);
-            r = q.rcap;
-            w = q.head;
-            rv = q.rev;
-            uc = q.ucap;
-            cr = q.cost + pv - P[w - k.x0];
+    for (int base = b0; base < en; base += CT * UC) {
+        int4 qr[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int a = base + CT * u + (int)threadIdx.x;
+            qr[u] = ld_raw(A, a < en ? a : b0);
         }
-        wcount(C_SCAN, valid);
-        const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
-        long long tot;
-        const long long excl = blk_excl_scan(adm, &tot);
-        long long d = rem - excl;
-        d = d < 0 ? 0 : (d > adm ? adm : d);
-        if (d > 0) push(A, k, nb, a, w, r, d, rv, uc);
-        wcount(C_PUSH, d > 0);
-        if (valid) {
-            if (cr < 0) {
-                if (r - d > 0) minc = min(minc, cr);
-            } else if (r > 0 || cr <= k.eps) {
-                minc = min(minc, cr);
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const Pos Q = dec(A, k, qr[u]);
+            const int a = base + CT * u + (int)threadIdx.x;
+            const bool valid = a < en;
+            int r = 0;
+            long long cr = 0;
+            if (valid) {
+                r = (int)Q.rcap;
+                cr = Q.cost + pv - P[Q.head - k.x0];
             }
+            t.c[C_SCAN] += valid;
+            const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
+            long long tot;
+            const long long excl = blk_excl_scan(adm, &tot);
+            long long d = rem - excl;
+            d = d < 0 ? 0 : (d > adm ? adm : d);
+            if (d > 0) {
+                push(A, k, nb, a, Q.head, r, d, Q.rev, Q.ucap);
+                ++t.c[C_PUSH];
+            }
+            minc_acc(minc, valid, cr, r, (int)d, k.eps);
+            rem -= tot < rem ? tot : rem;
         }
-        rem -= tot < rem ? tot : rem;
         if (rem == 0) break;
     }
     minc = blk_min(minc);
-    wcount(C_RELABEL, threadIdx.x == 0 && rem > 0);
     if (threadIdx.x == 0) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
         if (rem > 0) {
+            ++t.c[C_RELABEL];
             if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
             else relabel(A, k, v, pv - (minc + k.eps));
             mark(A, k, nb, v);
@@ -414,8 +510,7 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
 // and its reduced cost −(cost(a) + p(v) − p(u)). PR: price refinement (ε = 1,
 // negative lengths allowed, no clamp at 0).
 template <bool PR>
-__device__ __forceinline__ void relax(const CellArgs& A, const K& k, int nb, int a, int dv, long long pv) {
-    const Pos q = ld_pos(A.pos + a);
+__device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, const Pos& q, int dv, long long pv) {
     if (q.ucap - q.rcap <= 0) return;
     const int lu = q.head - k.x0;
     const long long pu = prc()[lu];
@@ -436,221 +531,382 @@ __device__ __forceinline__ void relax(const CellArgs& A, const K& k, int nb, int
     }
 }
 
-template <int G, bool PR>
-__device__ __forceinline__ void bf_grp(const CellArgs& A, K& k, int nb, int v) {
-    const int lig = lane() & (G - 1);
-    int dv = DINF;
-    long long pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        dv = dst(k)[v - k.x0];
-        pv = prc()[v - k.x0];
-        seg(A, v, b0, en);
-    }
-    if (!PR && dv >= DINF) en = b0;
-    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
-    for (int it = 0; it < iters; ++it) {
-        const int a = b0 + it * G + lig;
-        if (a < en) relax<PR>(A, k, nb, a, dv, pv);
-        wcount(C_GUSCAN, a < en);
-    }
-}
-
-template <bool PR>
-__device__ __forceinline__ void bf_hub(const CellArgs& A, K& k, int nb, int v) {
+// One node's in-arcs by one wave (W = 64, v uniform) or the workgroup (W = CT).
+template <int W, bool PR>
+__device__ __forceinline__ void bf_node(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const int dv = dst(k)[v - k.x0];
-    const long long pv = prc()[v - k.x0];
     if (!PR && dv >= DINF) return;
+    const long long pv = prc()[v - k.x0];
     int b0, en;
     seg(A, v, b0, en);
-    for (int base = b0; base < en; base += CT) {   // (a uniform trip count: the ballot needs the whole wave)
-        const int a = base + (int)threadIdx.x;
-        if (a < en) relax<PR>(A, k, nb, a, dv, pv);
-        wcount(C_GUSCAN, a < en);
+    const int me = W == 64 ? lane() : (int)threadIdx.x;
+    for (int base = b0 + me; base < en; base += W * UC) {
+        int4 qr[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u)
+            qr[u] = ld_raw(A, base + W * u < en ? base + W * u : base);
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const Pos Q = dec(A, k, qr[u]);
+            if (base + W * u < en) {
+                relax_q<PR>(A, k, nb, Q, dv, pv);
+                ++t.c[C_GUSCAN];
+            }
+        }
     }
 }
 
 // -------------------------------------------------------------- saturate ---
 // Goldberg's refine start: every residual arc of reduced cost below −thr is
-// saturated (thr = ε after a failed refinement or on a warm start).
-template <int G>
-__device__ __forceinline__ void sat_grp(const CellArgs& A, K& k, int v, long long thr) {
-    const long long* P = prc();
-    const int lig = lane() & (G - 1);
-    long long pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        pv = P[v - k.x0];
-        seg(A, v, b0, en);
-    }
-    const int iters = G < 64 ? 1 : (en - b0 + 63) / 64;
-    long long tot = 0;
-    for (int it = 0; it < iters; ++it) {
-        const int a = b0 + it * G + lig;
-        bool pushed = false;
-        if (a < en) {
-            const Pos q = ld_pos(A.pos + a);
-            if (q.rcap > 0 && q.cost + pv - P[q.head - k.x0] < -thr) {
-                A.pos[a].rcap = 0;
-                A.pos[q.rev].rcap = q.ucap;
-                add_ex(A, q.head, q.rcap);
-                tot += q.rcap;
-                pushed = true;
-            }
-        }
-        wcount(C_PUSH, pushed);
-    }
-    tot = g_sum<G>(tot);
-    if (v >= 0 && lig == 0 && tot) add_ex(A, v, -tot);
-}
-
-__device__ __forceinline__ void sat_hub(const CellArgs& A, K& k, int v, long long thr) {
+// saturated (thr = ε after a failed refinement or on a warm start). W as bf_node.
+template <int W>
+__device__ __forceinline__ void sat_node(const CellArgs& A, K& k, int v, long long thr, Tc& t) {
     const long long* P = prc();
     const long long pv = P[v - k.x0];
     int b0, en;
     seg(A, v, b0, en);
+    const int me = W == 64 ? lane() : (int)threadIdx.x;
     long long tot = 0;
-    for (int base = b0; base < en; base += CT) {
-        const int a = base + (int)threadIdx.x;
-        bool pushed = false;
-        if (a < en) {
-            const Pos q = ld_pos(A.pos + a);
-            if (q.rcap > 0 && q.cost + pv - P[q.head - k.x0] < -thr) {
-                A.pos[a].rcap = 0;
-                A.pos[q.rev].rcap = q.ucap;
-                add_ex(A, q.head, q.rcap);
-                tot += q.rcap;
-                pushed = true;
+    for (int base = b0 + me; base < en; base += W * UC) {
+        int4 qr[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u)
+            qr[u] = ld_raw(A, base + W * u < en ? base + W * u : base);
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const Pos Q = dec(A, k, qr[u]);
+            const int a = base + W * u;
+            if (a < en && Q.rcap > 0 && Q.cost + pv - P[Q.head - k.x0] < -thr) {
+                st_rcap(A, a, 0);
+                st_rcap(A, Q.rev, Q.ucap);
+                add_ex(A, Q.head, Q.rcap);
+                tot += Q.rcap;
+                ++t.c[C_PUSH];
             }
         }
-        wcount(C_PUSH, pushed);
     }
-    tot = blk_sum(tot);
-    if (threadIdx.x == 0 && tot) add_ex(A, v, -tot);
+    if (W == 64) {
+        tot = lane63_64(g_sum<64>(tot));
+        if (lane() == 0 && tot) add_ex(A, v, -tot);
+    } else {
+        tot = blk_sum(tot);
+        if (threadIdx.x == 0 && tot) add_ex(A, v, -tot);
+    }
+}
+
+// ------------------------------------------------ leaf classes, U at a time ---
+// Classes of ≤ 32 positions (PUs, tasks, machines): one node per G-lane group, one
+// position per lane (a task's eight 16-B records are one coalesced line), and U
+// batches of 64/G nodes in flight per wave: every batch's list, segment and
+// position loads are issued before any of them is used (one batch per wave left
+// each wave one dependent chain at a time — latency-bound at ~1.5 µs per batch).
+template <int G>
+struct LeafU {
+    static constexpr int U = G <= 16 ? 4 : 2;
+};
+
+// A batch's segment and record loads, all unconditional (indices clamped to the
+// cell's first node / position 0, masked after): a load inside a lane-conditional
+// branch gets its own s_waitcnt there, which serialises the batch.
+template <int G, int U>
+__device__ __forceinline__ void leaf_load(const CellArgs& A, const K& k, int lig, const int (&v)[U], int (&b0)[U],
+                                          int (&en)[U], int4 (&qr)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        seg(A, v[u] >= 0 ? v[u] : k.x0, b0[u], en[u]);
+        if (v[u] < 0) en[u] = b0[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int a = b0[u] + lig;
+        qr[u] = ld_raw(A, a < en[u] ? a : 0);
+    }
+}
+
+template <int G, int U>
+__device__ __forceinline__ void sweep_leaf(const CellArgs& A, K& k, int nb, const int (&v)[U], Tc& t) {
+    const long long* P = prc();
+    const int lig = lane() & (G - 1);
+    const bool lead = lig == G - 1;
+    long long e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u] = ld_ex(A, v[u] >= 0 ? v[u] : k.x0);
+    int b0[U], en[U];
+    int4 qr[U];
+    leaf_load<G, U>(A, k, lig, v, b0, en, qr);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (v[u] < 0) e[u] = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const Pos Q = dec(A, k, qr[u]);
+        const bool act = e[u] > 0;
+        const int a = b0[u] + lig;
+        const bool valid = act && a < en[u];
+        const long long pv = v[u] >= 0 ? P[v[u] - k.x0] : 0;
+        int r = 0;
+        long long cr = 0;
+        if (valid) {
+            r = (int)Q.rcap;
+            cr = Q.cost + pv - P[Q.head - k.x0];
+        }
+        t.c[C_SCAN] += valid;
+        t.c[C_VISIT] += act && lead;
+        const int adm = (valid && cr < 0 && r > 0) ? r : 0;
+        const int incl = gs_add<G>(adm, lig);                       // the last lane: the group's admissible total
+        const long long ex = e[u] - (incl - adm);              // what is left when this arc's turn comes
+        const int d = ex <= 0 ? 0 : (ex < adm ? (int)ex : adm);
+        if (d > 0) {
+            push(A, k, nb, a, Q.head, r, d, Q.rev, Q.ucap);
+            ++t.c[C_PUSH];
+        }
+        long long minc = INF64;
+        if (valid) {
+            if (cr < 0) {
+                if (r - d > 0) minc = cr;
+            } else if (r > 0 || cr <= k.eps) {
+                minc = cr;
+            }
+        }
+        minc = gs_min<G>(minc, lig);                                // the last lane: the group minimum
+        if (act && lead) {
+            const long long rem = e[u] > incl ? e[u] - incl : 0;
+            const long long pushed = e[u] - rem;
+            if (pushed) add_ex(A, v[u], -pushed);
+            if (rem > 0) {
+                ++t.c[C_RELABEL];
+                if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
+                else relabel(A, k, v[u], pv - (minc + k.eps));
+                mark(A, k, nb, v[u]);
+            }
+        }
+    }
+}
+
+template <int G, int U, bool PR>
+__device__ __forceinline__ void bf_leaf(const CellArgs& A, K& k, int nb, const int (&v)[U], Tc& t) {
+    const int lig = lane() & (G - 1);
+    int b0[U], en[U];
+    int4 qr[U];
+    leaf_load<G, U>(A, k, lig, v, b0, en, qr);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const Pos Q = dec(A, k, qr[u]);
+        if (b0[u] + lig >= en[u]) continue;
+        const int dv = dst(k)[v[u] - k.x0];
+        if (!PR && dv >= DINF) continue;
+        relax_q<PR>(A, k, nb, Q, dv, prc()[v[u] - k.x0]);
+        ++t.c[C_GUSCAN];
+    }
+}
+
+template <int G, int U>
+__device__ __forceinline__ void sat_leaf(const CellArgs& A, K& k, const int (&v)[U], long long thr, Tc& t) {
+    const long long* P = prc();
+    const int lig = lane() & (G - 1);
+    int b0[U], en[U];
+    int4 qr[U];
+    leaf_load<G, U>(A, k, lig, v, b0, en, qr);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const Pos Q = dec(A, k, qr[u]);
+        const int a = b0[u] + lig;
+        int tot = 0;
+        if (a < en[u]) {
+            const long long pv = P[v[u] - k.x0];
+            if (Q.rcap > 0 && Q.cost + pv - P[Q.head - k.x0] < -thr) {
+                st_rcap(A, a, 0);
+                st_rcap(A, Q.rev, Q.ucap);
+                add_ex(A, Q.head, Q.rcap);
+                tot = (int)Q.rcap;
+                ++t.c[C_PUSH];
+            }
+        }
+        tot = gs_add<G>(tot, lig);
+        if (v[u] >= 0 && lig == G - 1 && tot) add_ex(A, v[u], -(long long)tot);
+    }
 }
 
 // ------------------------------------------------ one thread per node ---
-// Classes of ≤ 32 positions (tasks, PUs, machines): a node per thread, its
-// positions loaded CH at a time (independent loads in flight), the excess spread
-// along them in order — the same distribution as the lane-group prefix sum, with
-// no cross-lane exchange, and 64 nodes per wave instead of 64/G.
-constexpr int CH = 4;
+// Classes of ≤ 4 and ≤ 8 positions (PUs, tasks): a node per thread, 64 per wave.
+// A cheap pass over all of a node's records (loaded at once, unconditionally)
+// builds a bitmask of the positions that need the expensive path — a push, a
+// relaxation, a saturation — and a ctz loop then takes only those, re-reading the
+// record (an L1 hit). A task has about one such position, so a wave runs the
+// expensive path about once per 64 tasks instead of once per position index
+// (the cell solve is VALU-bound on its CU: DESIGN §3.5).
+template <int MAXP>
+__device__ __forceinline__ int thr_load(const CellArgs& A, const K& k, int v, int& b0, int4 (&qr)[MAXP]) {
+    int en;
+    seg(A, v >= 0 ? v : k.x0, b0, en);
+    const int cnt = v >= 0 ? en - b0 : 0;
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) qr[i] = ld_raw(A, i < cnt ? b0 + i : 0);
+    return cnt;
+}
 
+template <int MAXP>
 __device__ __forceinline__ void sweep_thr(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const long long* P = prc();
-    long long e = 0, pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        e = ld_ex(A, v);
-        pv = P[v - k.x0];
-        seg(A, v, b0, en);
-    }
+    const long long e0 = ld_ex(A, v >= 0 ? v : k.x0);
+    int b0;
+    int4 qr[MAXP];
+    const int cnt = thr_load<MAXP>(A, k, v, b0, qr);
+    const long long e = v >= 0 ? e0 : 0;
     if (e <= 0) return;
+    const long long pv = P[v - k.x0];
     ++t.c[C_VISIT];
+    t.c[C_SCAN] += cnt;
     long long rem = e, minc = INF64;
-    for (int a0 = b0; a0 < en; a0 += CH) {
-        Pos q[CH];
+    unsigned pm = 0;   // positions that receive a push
 #pragma unroll
-        for (int u = 0; u < CH; ++u)
-            if (a0 + u < en) q[u] = ld_pos(A.pos + a0 + u);
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            if (a0 + u >= en) break;
-            ++t.c[C_SCAN];
-            const long long r = q[u].rcap;
-            const long long cr = q[u].cost + pv - P[q[u].head - k.x0];
-            long long d = 0;
-            if (cr < 0 && r > 0) {
-                d = rem < r ? rem : r;
-                if (d > 0) {
-                    push(A, k, nb, a0 + u, q[u].head, r, d, q[u].rev, q[u].ucap);
-                    ++t.c[C_PUSH];
-                    rem -= d;
-                }
+    for (int i = 0; i < MAXP; ++i) {
+        if (i >= cnt) break;
+        const Pos Q = dec(A, k, qr[i]);
+        const int r = (int)Q.rcap;
+        const long long cr = Q.cost + pv - P[Q.head - k.x0];
+        if (cr < 0) {   // admissible when residual (the relabel minimum as in sweep_leaf)
+            if (r > 0) {
+                const long long d = rem < r ? rem : r;
+                if (d > 0) pm |= 1u << i;
+                rem -= d;
                 if (r - d > 0) minc = min(minc, cr);
-            } else if (r > 0 || cr <= k.eps) {
-                minc = min(minc, cr);
             }
+        } else if (r > 0 || cr <= k.eps) {
+            minc = min(minc, cr);
         }
-        if (rem == 0) break;
+    }
+    long long left = e;
+    while (pm) {   // in position order: the same amounts as above (an admissible arc is
+                   // not changed by another node's push within the sweep)
+        const int i = __builtin_ctz(pm);
+        pm &= pm - 1;
+        const int a = b0 + i;
+        const Pos Q = ld_cp(A, k, a);
+        const int r = (int)Q.rcap;
+        const int d = left < r ? (int)left : r;
+        left -= d;
+        push(A, k, nb, a, Q.head, r, d, Q.rev, Q.ucap);
+        ++t.c[C_PUSH];
     }
     const long long pushed = e - rem;
     if (pushed) add_ex(A, v, -pushed);
     if (rem > 0) {
+        ++t.c[C_RELABEL];
         if (minc >= INF64) atomicOr(&s_.flag, F_INFEAS);
         else relabel(A, k, v, pv - (minc + k.eps));
-        ++t.c[C_RELABEL];
         mark(A, k, nb, v);
     }
 }
 
-template <bool PR>
+template <int MAXP, bool PR>
 __device__ __forceinline__ void bf_thr(const CellArgs& A, K& k, int nb, int v, Tc& t) {
-    int dv = DINF;
-    long long pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        dv = dst(k)[v - k.x0];
-        pv = prc()[v - k.x0];
-        seg(A, v, b0, en);
-    }
-    if (!PR && dv >= DINF) return;
-    for (int a0 = b0; a0 < en; a0 += CH) {
+    const int vc = v >= 0 ? v : k.x0;
+    const int dv = dst(k)[vc - k.x0];
+    int b0;
+    int4 qr[MAXP];
+    int cnt = thr_load<MAXP>(A, k, v, b0, qr);
+    if (!PR && dv >= DINF) cnt = 0;
+    t.c[C_GUSCAN] += cnt;
+    unsigned m = 0;   // positions whose reverse (an in-arc of v) is residual
 #pragma unroll
-        for (int u = 0; u < CH; ++u)
-            if (a0 + u < en) {
-                relax<PR>(A, k, nb, a0 + u, dv, pv);
-                ++t.c[C_GUSCAN];
-            }
+    for (int i = 0; i < MAXP; ++i)
+        if (i < cnt && qr[i].y - qr[i].x > 0) m |= 1u << i;
+    if (!m) return;
+    const long long pv = prc()[vc - k.x0];
+    while (m) {
+        const int i = __builtin_ctz(m);
+        m &= m - 1;
+        relax_q<PR>(A, k, nb, ld_cp(A, k, b0 + i), dv, pv);
     }
 }
 
+template <int MAXP>
 __device__ __forceinline__ void sat_thr(const CellArgs& A, K& k, int v, long long thr, Tc& t) {
     const long long* P = prc();
-    long long pv = 0;
-    int b0 = 0, en = 0;
-    if (v >= 0) {
-        pv = P[v - k.x0];
-        seg(A, v, b0, en);
+    int b0;
+    int4 qr[MAXP];
+    const int cnt = thr_load<MAXP>(A, k, v, b0, qr);
+    if (!cnt) return;
+    const long long pv = P[v - k.x0];
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+        if (i >= cnt) break;
+        const Pos Q = dec(A, k, qr[i]);
+        if (Q.rcap > 0 && Q.cost + pv - P[Q.head - k.x0] < -thr) m |= 1u << i;
     }
     long long tot = 0;
-    for (int a0 = b0; a0 < en; a0 += CH) {
-        Pos q[CH];
-#pragma unroll
-        for (int u = 0; u < CH; ++u)
-            if (a0 + u < en) q[u] = ld_pos(A.pos + a0 + u);
-#pragma unroll
-        for (int u = 0; u < CH; ++u)
-            if (a0 + u < en && q[u].rcap > 0 && q[u].cost + pv - P[q[u].head - k.x0] < -thr) {
-                A.pos[a0 + u].rcap = 0;
-                A.pos[q[u].rev].rcap = q[u].ucap;
-                add_ex(A, q[u].head, q[u].rcap);
-                tot += q[u].rcap;
-                ++t.c[C_PUSH];
-            }
+    while (m) {
+        const int i = __builtin_ctz(m);
+        m &= m - 1;
+        const int a = b0 + i;
+        const Pos Q = ld_cp(A, k, a);
+        st_rcap(A, a, 0);
+        st_rcap(A, Q.rev, Q.ucap);
+        add_ex(A, Q.head, Q.rcap);
+        tot += Q.rcap;
+        ++t.c[C_PUSH];
     }
     if (tot) add_ex(A, v, -tot);
 }
 
 // ------------------------------------------------------------------ step ---
-// An item: 64 nodes of a class ≤ 32 positions (one per thread), or one node of
-// the ≤ 64 / ≤ 512-position classes (the wave).
+constexpr int THR_CLASSES = 2;   // classes 0, 1: a node per thread; 2, 3: a lane group per node
+__host__ __device__ constexpr int items_per_wave(int c) {   // leaf nodes per item
+    return c < THR_CLASSES ? 64 : c < 4 ? (64 / (4 << c)) * ((4 << c) <= 16 ? 4 : 2) : 1;
+}
+
+// An item: a batch of leaf-class nodes, or one node of the ≤ 64 / ≤ 512-position
+// classes (the wave).
 template <int OP, int C>
 __device__ __forceinline__ void item(const CellArgs& A, K& k, int src, int nb, int j, int n, long long thr, Tc& t) {
-    if (C < 4) {
+    if (C < THR_CLASSES) {
         const int idx = j * 64 + lane();
-        const int v = idx < n ? node_at(A, src, C, idx) : -1;
-        if (OP == OP_SWEEP) sweep_thr(A, k, nb, v, t);
-        else if (OP == OP_BF) bf_thr<false>(A, k, nb, v, t);
-        else if (OP == OP_PR) bf_thr<true>(A, k, nb, v, t);
-        else sat_thr(A, k, v, thr, t);
+        int v;
+        if (src == 2) v = idx < n ? s_.cbs[C] + idx : -1;
+        else {
+            const int x = A.lists[(size_t)src * A.nn + s_.cbs[C] + (idx < n ? idx : 0)];
+            v = idx < n ? x : -1;
+        }
+        constexpr int MAXP = 4 << C;
+        if (OP == OP_SWEEP) sweep_thr<MAXP>(A, k, nb, v, t);
+        else if (OP == OP_BF) bf_thr<MAXP, false>(A, k, nb, v, t);
+        else if (OP == OP_PR) bf_thr<MAXP, true>(A, k, nb, v, t);
+        else sat_thr<MAXP>(A, k, v, thr, t);
+        return;
+    }
+    if (C < 4) {
+        constexpr int G = 4 << C;
+        constexpr int U = LeafU<G>::U;
+        int v[U];
+        const int grp = lane() / G;
+        if (src == 2) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = (j * U + u) * (64 / G) + grp;
+                v[u] = idx < n ? s_.cbs[C] + idx : -1;
+            }
+        } else {   // the list loads unconditional and outside any per-batch branch (see leaf_load)
+            const int* L = A.lists + (size_t)src * A.nn + s_.cbs[C];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = (j * U + u) * (64 / G) + grp;
+                const int x = L[idx < n ? idx : 0];
+                v[u] = idx < n ? x : -1;
+            }
+        }
+        if (OP == OP_SWEEP) sweep_leaf<G, U>(A, k, nb, v, t);
+        else if (OP == OP_BF) bf_leaf<G, U, false>(A, k, nb, v, t);
+        else if (OP == OP_PR) bf_leaf<G, U, true>(A, k, nb, v, t);
+        else sat_leaf<G, U>(A, k, v, thr, t);
         return;
     }
     const int v = __builtin_amdgcn_readfirstlane(node_at(A, src, C, j));
-    if (OP == OP_SWEEP) sweep_grp<64>(A, k, nb, v);
-    else if (OP == OP_BF) bf_grp<64, false>(A, k, nb, v);
-    else if (OP == OP_PR) bf_grp<64, true>(A, k, nb, v);
-    else sat_grp<64>(A, k, v, thr);
+    if (OP == OP_SWEEP) sweep_wave(A, k, nb, v, t);
+    else if (OP == OP_BF) bf_node<64, false>(A, k, nb, v, t);
+    else if (OP == OP_PR) bf_node<64, true>(A, k, nb, v, t);
+    else sat_node<64>(A, k, v, thr, t);
 }
 
 // One step over frontier src (2: every node) into buffer nb: the workgroup-
@@ -659,33 +915,56 @@ __device__ __forceinline__ void item(const CellArgs& A, K& k, int src, int nb, i
 // 16 waves. The caller's barrier completes buffer nb; step_post then empties src.
 template <int OP>
 __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, long long thr) {
+    Tc t;
     const int n6 = count_of(src, 6);
     for (int j = 0; j < n6; ++j) {
         const int v = node_at(A, src, 6, j);
         __syncthreads();   // the previous node's pushes and marks are in
-        if (OP == OP_SWEEP) sweep_hub(A, k, nb, v);
-        else if (OP == OP_BF) bf_hub<false>(A, k, nb, v);
-        else if (OP == OP_PR) bf_hub<true>(A, k, nb, v);
-        else sat_hub(A, k, v, thr);
+        const unsigned long long h0 = __builtin_amdgcn_s_memrealtime();
+        if (OP == OP_SWEEP) sweep_hub(A, k, nb, v, t);
+        else if (OP == OP_BF) bf_node<CT, false>(A, k, nb, v, t);
+        else if (OP == OP_PR) bf_node<CT, true>(A, k, nb, v, t);
+        else sat_node<CT>(A, k, v, thr, t);
+        if (threadIdx.x == 0) {
+            atomicAdd(&cls_t_[OP][6], __builtin_amdgcn_s_memrealtime() - h0);
+            atomicAdd(&cls_n_[OP][6], 1u);
+        }
     }
     const int n0 = count_of(src, 0), n1 = count_of(src, 1), n2 = count_of(src, 2), n3 = count_of(src, 3),
               n4 = count_of(src, 4), n5 = count_of(src, 5);
-    const int e0 = (n0 + 63) >> 6;
-    const int e1 = e0 + ((n1 + 63) >> 6);
-    const int e2 = e1 + ((n2 + 63) >> 6);
-    const int e3 = e2 + ((n3 + 63) >> 6);
-    const int e4 = e3 + n4;
-    const int e5 = e4 + n5;
-    Tc t;
-    for (int it = wid(); it < e5; it += NW) {
-        if (it < e0) item<OP, 0>(A, k, src, nb, it, n0, thr, t);
-        else if (it < e1) item<OP, 1>(A, k, src, nb, it - e0, n1, thr, t);
-        else if (it < e2) item<OP, 2>(A, k, src, nb, it - e1, n2, thr, t);
-        else if (it < e3) item<OP, 3>(A, k, src, nb, it - e2, n3, thr, t);
-        else if (it < e4) item<OP, 4>(A, k, src, nb, it - e3, n4, thr, t);
-        else item<OP, 5>(A, k, src, nb, it - e4, n5, thr, t);
+    constexpr int p0 = items_per_wave(0), p1 = items_per_wave(1), p2 = items_per_wave(2), p3 = items_per_wave(3);
+    // the costliest items first (an aggregator per wave, then machines, then
+    // batches of tasks), taken dynamically: the step's tail is its cheapest items
+    const int e5 = n5;
+    const int e4 = e5 + n4;
+    const int e3 = e4 + (n3 + p3 - 1) / p3;
+    const int e2 = e3 + (n2 + p2 - 1) / p2;
+    const int e1 = e2 + (n1 + p1 - 1) / p1;
+    const int e0 = e1 + (n0 + p0 - 1) / p0;
+    for (;;) {
+        int it0 = 0;
+        if (lane() == 0) it0 = atomicAdd(&s_.next, 1);
+        const int it = __builtin_amdgcn_readfirstlane(it0);
+        if (it >= e0) break;
+        const unsigned long long i0 = __builtin_amdgcn_s_memrealtime();
+        const int cl = it < e5 ? 5 : it < e4 ? 4 : it < e3 ? 3 : it < e2 ? 2 : it < e1 ? 1 : 0;
+        if (it < e5) item<OP, 5>(A, k, src, nb, it, n5, thr, t);
+        else if (it < e4) item<OP, 4>(A, k, src, nb, it - e5, n4, thr, t);
+        else if (it < e3) item<OP, 3>(A, k, src, nb, it - e4, n3, thr, t);
+        else if (it < e2) item<OP, 2>(A, k, src, nb, it - e3, n2, thr, t);
+        else if (it < e1) item<OP, 1>(A, k, src, nb, it - e2, n1, thr, t);
+        else item<OP, 0>(A, k, src, nb, it - e1, n0, thr, t);
+        if (lane() == 0) {
+            atomicAdd(&cls_t_[OP][cl], __builtin_amdgcn_s_memrealtime() - i0);
+            atomicAdd(&cls_n_[OP][cl], 1u);
+        }
     }
     flush(t);
+    if (lane() == 0) {   // when this wave's items were done (diagnostics: item span vs barrier tail)
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&t_items_, now);
+        atomicMin(&t_first_, now);
+    }
 }
 
 // After a step's barrier: src emptied; a sweep's relabels take effect; the
@@ -728,6 +1007,8 @@ struct Ctl {
     unsigned long long t_op;                // when the running operation started
     unsigned long long op_ticks[O_DONE];    // 100 MHz ticks per operation kind (incl. its barriers)
     unsigned op_n[O_DONE];
+    unsigned long long item_ticks[O_DONE];  // op start → the last wave's items done
+    unsigned long long first_ticks[O_DONE]; // op start → the first wave's items done
 };
 __shared__ Ctl c_;
 
@@ -772,10 +1053,15 @@ __device__ __forceinline__ void phase_end(const CellArgs& A) {
 
 __device__ __forceinline__ void control(const CellArgs& A, int N) {
     Ctl& c = c_;
+    s_.next = 0;   // the next step's item dispenser (read after the barrier that follows)
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     c.op_ticks[c.op] += now - c.t_op;
+    if (t_items_ > c.t_op) c.item_ticks[c.op] += t_items_ - c.t_op;
+    if (t_first_ > c.t_op && t_first_ != ~0ULL) c.first_ticks[c.op] += t_first_ - c.t_op;
     ++c.op_n[c.op];
-    c.t_op = now;
+    t_items_ = 0;
+    t_first_ = ~0ULL;
+    c.t_op = __builtin_amdgcn_s_memrealtime();
     if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
     switch (c.op) {
         case O_SAT:
@@ -923,16 +1209,32 @@ __device__ __forceinline__ void gu_fin(const CellArgs& A, const K& k) {
 __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
     const CellDesc cd = A.cells[blockIdx.x];
     const int N = cd.cb[CELL_NCLS] - cd.cb[0];
+    const int pb = A.first[cd.cb[0]];
     if (threadIdx.x < 8) s_.cbs[threadIdx.x] = A.cells[blockIdx.x].cb[threadIdx.x];
     if (threadIdx.x < NCTR) ctr_[threadIdx.x] = 0;
+    if (*A.bad) {   // a position the compact record cannot hold: nothing is touched
+        if (threadIdx.x == 0) {
+            CellOut o{};
+            o.status = CS_RANGE;
+            A.out[blockIdx.x] = o;
+        }
+        return;
+    }
     if (threadIdx.x == 0) {
         s_.rl_cnt[0] = s_.rl_cnt[1] = 0;
         s_.flag = 0;
         s_.stop = 0;
+        s_.next = 0;
         Ctl& c = c_;
         c = Ctl{};
         c.t0 = __builtin_amdgcn_s_memrealtime();
         c.t_op = c.t0;
+        t_items_ = 0;
+        t_first_ = ~0ULL;
+        for (int i = 0; i < 32; ++i) {
+            (&cls_t_[0][0])[i] = 0;
+            (&cls_n_[0][0])[i] = 0;
+        }
         c.eps_ph = A.eps_start;
         c.eps = 1;
         if (N == 0) {
@@ -973,6 +1275,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         k.N = N;
         k.maxn = A.max_nodes;
         k.W = (N + 31) / 32;
+        k.pb = pb;
         k.c1 = cd.cb[1];
         k.c2 = cd.cb[2];
         k.c3 = cd.cb[3];
@@ -1060,9 +1363,53 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         for (int i = 0; i < CELL_NOPS; ++i) {
             o.op_ticks[i] = c.op_ticks[i];
             o.op_n[i] = c.op_n[i];
+            o.item_ticks[i] = c.item_ticks[i];
+            o.first_ticks[i] = c.first_ticks[i];
+        }
+        for (int i = 0; i < 32; ++i) {
+            o.cls_ticks[i] = (&cls_t_[0][0])[i];
+            o.cls_n[i] = (&cls_n_[0][0])[i];
         }
         A.out[blockIdx.x] = o;
     }
+}
+
+// Grid-wide, before the cell launch: every position's compact record. The head's
+// cell (a binary search over the cells' first ids) gives the local head index and
+// the base of the reverse's offset. A value the record cannot hold flags *bad, and
+// the cells then return CS_RANGE without touching anything (the host falls back
+// to the multi-kernel engine).
+__global__ void k_cell_pack(CellArgs A, int* bad) {
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < A.m2; p += (long long)gridDim.x * blockDim.x) {
+        const Pos q = ld_pos(A.pos + p);
+        int lo = 0, hi = A.ncells;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (A.cells[mid].cb[0] <= q.head) lo = mid;
+            else hi = mid;
+        }
+        const int x0 = A.cells[lo].cb[0];
+        const long long pb = A.first[x0];
+        CellPos c;
+        const bool dead = q.cost >= DEAD_SCALED;
+        const long long cu = dead ? 0 : q.cost / A.mult;
+        const long long hl = q.head - x0, rr = q.rev - pb;
+        if (q.ucap > CELL_MAX_CAP || q.rcap > CELL_MAX_CAP || cu > CELL_MAX_COST || cu < -CELL_MAX_COST ||
+            hl >= (1LL << CELL_HEAD_BITS) || rr < 0 || rr >= CELL_MAX_POS)
+            atomicOr(bad, 1);
+        c.rcap = (int)q.rcap;
+        c.ucap = (int)q.ucap;
+        c.cost = dead ? CELL_DEAD : (int)cu;
+        c.hr = (unsigned)hl | ((unsigned)rr << CELL_HEAD_BITS);
+        A.cp[p] = c;
+    }
+}
+
+// After the cell launch: the residuals back into the engine's positions.
+__global__ void k_cell_unpack(CellArgs A, const int* bad) {
+    if (*bad) return;
+    for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < A.m2; p += (long long)gridDim.x * blockDim.x)
+        A.pos[p].rcap = A.cp[p].rcap;
 }
 
 }  // namespace
@@ -1073,7 +1420,7 @@ size_t cell_lds_bytes(int n) {
     // prices 8n, distances 4n rounded up to whole 8-byte words, two bitmaps
     const size_t b = 8 * (size_t)n + 8 * (((size_t)n + 1) / 2) + 2 * 4 * w;
     const size_t dyn = (b + 15) / 16 * 16;
-    return dyn + sizeof(St) + sizeof(Ctl) + 64 <= LDS_LIMIT ? dyn : 0;
+    return dyn + sizeof(St) + sizeof(Ctl) + 64 + sizeof(cls_t_) + sizeof(cls_n_) <= LDS_LIMIT ? dyn : 0;
 }
 
 int cell_max_nodes() {
@@ -1086,14 +1433,20 @@ int cell_max_nodes() {
     return lo;
 }
 
-hipError_t cell_launch(const CellArgs& a, hipStream_t st) {
+hipError_t cell_launch(const CellArgs& a, int* bad, hipStream_t st) {
     const size_t lds = cell_lds_bytes(a.max_nodes);
     if (!lds || a.ncells <= 0) return hipErrorInvalidValue;
     // (per device and cheap: set on every launch)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cell),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cell),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_cell, dim3(a.ncells), dim3(CT), lds, st, a);
+    if ((e = hipMemsetAsync(bad, 0, sizeof(int), st)) != hipSuccess) return e;
+    const int pg = (int)std::min<long long>(4096, (a.m2 + 255) / 256 > 0 ? (a.m2 + 255) / 256 : 1);
+    hipLaunchKernelGGL(k_cell_pack, dim3(pg), dim3(256), 0, st, a, bad);
+    CellArgs b = a;
+    b.bad = bad;
+    hipLaunchKernelGGL(k_cell, dim3(a.ncells), dim3(CT), lds, st, b);
+    hipLaunchKernelGGL(k_cell_unpack, dim3(pg), dim3(256), 0, st, a, (const int*)bad);
     return hipGetLastError();
 }
 

@@ -2844,6 +2844,9 @@ struct EngineImpl {
     DBuf<int> cl_lists, cl_rln;
     DBuf<long long> cl_rlp;
     DBuf<CellOut> cl_out;
+    DBuf<CellPos> cl_pos;               // compact positions (k_cell_pack / k_cell_unpack)
+    DBuf<int> cl_bad;
+    bool cell_refused = false;          // the graph's values do not fit the compact record: engine until reload
     std::vector<CellOut> h_cell_out;
     // ---- scheduler-side sweeps (ks_sched.hip)
     DBuf<int> sched_i;                  // int scratch
@@ -2897,7 +2900,8 @@ struct EngineImpl {
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
-        cells.release(); cl_lists.release(); cl_rln.release(); cl_rlp.release(); cl_out.release();
+        cells.release(); cl_lists.release(); cl_rln.release(); cl_rlp.release(); cl_out.release(); cl_pos.release();
+        cl_bad.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         for (auto* h : h_cyc)
             if (h) (void)hipHostFree(h);
@@ -3206,6 +3210,7 @@ int Engine::load(int64_t nslots, const int64_t* supply, const uint8_t* type, con
     s.rebuilds = 0;
     s.solved = false;
     s.has_prev = false;
+    s.cell_refused = false;
     rc = ensure_arcs(s, (int64_t)m, err);
     if (rc) return rc;
     if (s.hcap) {   // clear the index (keeps its size)
@@ -3307,6 +3312,7 @@ static int cell_order(EngineImpl& s, int64_t ncap, std::string& err) {
     KS_CHECK(s.cl_rln.ensure(std::max(nn, 1)));
     KS_CHECK(s.cl_rlp.ensure(std::max(nn, 1)));
     KS_CHECK(s.cl_out.ensure(k));
+    KS_CHECK(s.cl_bad.ensure(1));
     s.h_cell_out.resize(k);
     return KS_OK;
 }
@@ -3542,7 +3548,7 @@ void Engine::set_cells(const int64_t* off, size_t k) {
 // graph) fits one workgroup's LDS and ks_opts.cell_nodes allows it. Sizes are node
 // slots as the build lays them out (the current build's, or the next one's).
 static bool want_cells(const EngineImpl& s) {
-    if (s.opts.cell_nodes < 0) return false;
+    if (s.opts.cell_nodes < 0 || s.cell_refused) return false;
     const int64_t lim = std::min<int64_t>(cell_max_nodes(), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
     const int64_t ncap =
         s.csr_valid ? s.ncap : s.nslots + (s.incremental ? std::max<int64_t>(64, s.nslots / 16) : 0);
@@ -4368,6 +4374,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     auto run_cells = [&](int mode) -> int {
         CellArgs a{};
         a.pos = s.pos.p;
+        a.cp = s.cl_pos.p;
+        a.first = s.first.p;
+        a.m2 = (int)s.m2cap;
         a.nd = s.nd.p;
         a.excess = s.excess.p;
         a.cells = s.cells.p;
@@ -4392,12 +4401,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.max_nodes = s.cell_max;
         a.timeout_ticks = (unsigned long long)(kCellLimitS * 1e8);
         KS_CHECK(hipEventRecord(s.kev[2], st));
-        KS_CHECK(cell_launch(a, st));
+        KS_CHECK(cell_launch(a, s.cl_bad.p, st));
         KS_CHECK(hipEventRecord(s.kev[3], st));
         KS_CHECK(hipMemcpyAsync(s.h_cell_out.data(), s.cl_out.p, ncells * sizeof(CellOut), hipMemcpyDeviceToHost, st));
         KS_CHECK(hipStreamSynchronize(st));
         ms_cell += ev_ms(s.kev[2], s.kev[3]);
         int worst = CS_OK, pmax = 0;
+        for (const CellOut& o : s.h_cell_out)
+            if (o.status == CS_RANGE) return (int)CS_RANGE;
         for (const CellOut& o : s.h_cell_out) {
             if (o.status != CS_OK && (worst == CS_OK || worst == CS_INFEASIBLE)) worst = o.status;
             pmax = std::max(pmax, o.phases);
@@ -4423,7 +4434,17 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                          o.ticks / 1e5, o.phases, o.updates, o.sweeps, o.bf_rounds);
             for (int i = 0; i < CELL_NOPS; ++i)
                 if (o.op_n[i])
-                    std::fprintf(stderr, " %s %u x %.2f us", names[i], o.op_n[i], o.op_ticks[i] / 100.0 / o.op_n[i]);
+                    std::fprintf(stderr, " %s %u x %.2f us (items %.2f..%.2f)", names[i], o.op_n[i],
+                                 o.op_ticks[i] / 100.0 / o.op_n[i], o.first_ticks[i] / 100.0 / o.op_n[i],
+                                 o.item_ticks[i] / 100.0 / o.op_n[i]);
+            static const char* const steps[4] = {"sweep", "bf", "pr", "sat"};
+            for (int s = 0; s < 4; ++s) {
+                std::fprintf(stderr, "\n  %s items:", steps[s]);
+                for (int c = 0; c < 7; ++c)
+                    if (o.cls_n[8 * s + c])
+                        std::fprintf(stderr, " c%d %u x %.2f us", c, o.cls_n[8 * s + c],
+                                     o.cls_ticks[8 * s + c] / 100.0 / o.cls_n[8 * s + c]);
+            }
             std::fprintf(stderr, "\n");
         }
         return worst;
@@ -4440,9 +4461,16 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         return KS_E_DEVICE;
     };
     if (s.cell_layout) {
+        KS_CHECK(s.cl_pos.ensure(std::max<int64_t>(m2, 1)));
         KS_CHECK(hipEventRecord(s.ev[3], st));
         const int cs = run_cells(0);
         if (cs < 0) return cs;
+        if (cs == CS_RANGE) {   // a value the compact record cannot hold: the multi-kernel engine instead
+            s.cell_refused = true;
+            s.cell_layout = false;
+            s.csr_valid = false;
+            return solve(res, warm, err);
+        }
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
         ms_cycles += ev_ms(s.ev[3], s.ev[5]);

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--engine", type=int, default=1, help="also time the multi-kernel engine")
     ap.add_argument("--min-n", type=int, default=0)
     ap.add_argument("--log", type=int, default=0, help="ks_opts.log_cycles on the cell path (per-op times on stderr)")
+    ap.add_argument("--opts", default="{}", help="JSON ks_opts overrides for the cell path, e.g. '{\"gu_interval\": 48}'")
     args = ap.parse_args()
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "goldens.json")))["graphs"]
     sel = [e for e in gold if args.min_n <= e["n"] <= 14000][: args.graphs]
@@ -40,7 +41,7 @@ def main():
     for e in sel:
         g = graph_of(e)
         row = {"family": e["family"], "params": e["params"], "seed": e["seed"], "n": g.n, "gold": e["cost"]}
-        for name, opts in (("cell", {"log_cycles": args.log}), ("engine", {"cell_nodes": -1})):
+        for name, opts in (("cell", {"log_cycles": args.log, **json.loads(args.opts)}), ("engine", {"cell_nodes": -1})):
             if name == "engine" and not args.engine:
                 continue
             ctx = native.Context(0, **opts)
