@@ -140,8 +140,10 @@ typedef struct ks_opts {
                                   The last phase always uses global updates. < 0 off      */
     int32_t  cell_nodes;       /* the cell solver (one workgroup per graph)
                                   solves every graph — or every cell of a ks_batch union —
-                                  of at most cell_nodes node slots [0: as many as its LDS
-                                  holds, 13,2xx]; < 0: always the multi-kernel engine    */
+                                  of at most cell_nodes node slots [0: a ks_batch cell up
+                                  to what its LDS holds (13,1xx), a lone graph up to 4,096
+                                  (larger ones solve sooner on the whole chip)]; < 0:
+                                  always the multi-kernel engine                          */
     int32_t  reserved[3];
 } ks_opts;
 

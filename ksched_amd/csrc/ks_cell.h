@@ -41,8 +41,8 @@ struct CellDesc {
 
 // The cell solver's 16-byte copy of a residual position (packed before a solve
 // from the 32-byte ks_pos.h record, its residual written back after): residual and
-// pair capacity (int32), the UNSCALED cost (int32; CELL_DEAD for an inert
-// position), the head as a cell-local node index (14 bits) and the reverse
+// pair capacity (int32), the SCALED cost (int32 — cost·(n+1) must fit, else the
+// solve falls back to the engine; CELL_DEAD for an inert position), the head as a cell-local node index (14 bits) and the reverse
 // position relative to the cell's first position (18 bits). A task's eight
 // positions are one 128-byte line instead of two.
 struct alignas(16) CellPos {
@@ -56,7 +56,7 @@ constexpr int CELL_MAX_POS = 1 << (32 - CELL_HEAD_BITS);   // positions per cell
 constexpr int CELL_DEAD = 0x7fffffff;                       // an inert position's cost
 constexpr long long CELL_MAX_CAP = (1LL << 24) - 1;         // capacities the cell solver takes (a lane group's
                                                             // admissible sum then fits int32) and |cost|
-constexpr long long CELL_MAX_COST = (1LL << 30) - 1;
+constexpr long long CELL_MAX_COST = (1LL << 31) - 2;        // |scaled cost| (CELL_DEAD = 2^31 − 1 marks inert)
 
 enum CellStatus { CS_OK = 0, CS_INFEASIBLE = 1, CS_NOCONV = 2, CS_TIMEOUT = 3, CS_RANGE = 4 };
 
@@ -80,6 +80,8 @@ struct CellOut {
     unsigned long long first_ticks[8];   //              op start → the first wave's items done
     unsigned long long cls_ticks[32];    //              item ticks by step (sweep, BF, refinement, saturate) × class
     unsigned cls_n[32];                  //              and items (class 6: the workgroup-sized nodes)
+    unsigned long long hist_t[12];       //              sweep (0–5) / BF round (6–11) ticks by frontier size
+    unsigned hist_n[12];                 //              (≤ 16, 64, 256, 1k, 4k, more nodes) and counts
 };
 constexpr int CELL_NOPS = 8;
 

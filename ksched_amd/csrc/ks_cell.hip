@@ -151,7 +151,7 @@ __device__ __forceinline__ Pos dec(const CellArgs& A, const K& k, int4 w) {
     Pos r;
     r.rcap = w.x;
     r.ucap = w.y;
-    r.cost = w.z == CELL_DEAD ? DEAD_SCALED : (long long)w.z * A.mult;
+    r.cost = w.z == CELL_DEAD ? DEAD_SCALED : (long long)w.z;
     r.head = k.x0 + (int)((unsigned)w.w & ((1u << CELL_HEAD_BITS) - 1));
     r.rev = k.pb + (int)((unsigned)w.w >> CELL_HEAD_BITS);
     return r;
@@ -448,8 +448,9 @@ __device__ __forceinline__ void sweep_wave(const CellArgs& A, K& k, int nb, int 
     }
 }
 
-// The same for a node above 512 positions: the whole workgroup, 1024 positions
-// per chunk, the excess spread by a workgroup-wide prefix sum. v is uniform.
+// The same for a node above 512 positions: the whole workgroup, each thread UC
+// consecutive positions (position order kept), one workgroup prefix sum per
+// CT·UC positions. v is uniform.
 __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const long long* P = prc();
     const long long e = ld_ex(A, v);
@@ -460,36 +461,37 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
     t.c[C_VISIT] += threadIdx.x == 0;
     long long rem = e, minc = INF64;
     for (int base = b0; base < en; base += CT * UC) {
+        const int a0 = base + (int)threadIdx.x * UC;
         int4 qr[UC];
 #pragma unroll
-        for (int u = 0; u < UC; ++u) {
-            const int a = base + CT * u + (int)threadIdx.x;
-            qr[u] = ld_raw(A, a < en ? a : b0);
-        }
+        for (int u = 0; u < UC; ++u) qr[u] = ld_raw(A, a0 + u < en ? a0 + u : b0);
+        long long cr[UC];
+        int adm[UC], my = 0;
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const Pos Q = dec(A, k, qr[u]);
-            const int a = base + CT * u + (int)threadIdx.x;
-            const bool valid = a < en;
-            int r = 0;
-            long long cr = 0;
-            if (valid) {
-                r = (int)Q.rcap;
-                cr = Q.cost + pv - P[Q.head - k.x0];
-            }
+            const bool valid = a0 + u < en;
+            cr[u] = valid ? Q.cost + pv - P[Q.head - k.x0] : 0;
+            adm[u] = (valid && cr[u] < 0 && Q.rcap > 0) ? (int)Q.rcap : 0;
+            my += adm[u];
             t.c[C_SCAN] += valid;
-            const long long adm = (valid && cr < 0 && r > 0) ? r : 0;
-            long long tot;
-            const long long excl = blk_excl_scan(adm, &tot);
-            long long d = rem - excl;
-            d = d < 0 ? 0 : (d > adm ? adm : d);
+        }
+        long long tot;
+        long long before = blk_excl_scan(my, &tot);
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const Pos Q = dec(A, k, qr[u]);
+            const int r = (int)Q.rcap;
+            long long d = rem - before;
+            d = d < 0 ? 0 : (d > adm[u] ? adm[u] : d);
+            before += adm[u];
             if (d > 0) {
-                push(A, k, nb, a, Q.head, r, d, Q.rev, Q.ucap);
+                push(A, k, nb, a0 + u, Q.head, r, d, Q.rev, Q.ucap);
                 ++t.c[C_PUSH];
             }
-            minc_acc(minc, valid, cr, r, (int)d, k.eps);
-            rem -= tot < rem ? tot : rem;
+            minc_acc(minc, a0 + u < en, cr[u], r, (int)d, k.eps);
         }
+        rem -= tot < rem ? tot : rem;
         if (rem == 0) break;
     }
     minc = blk_min(minc);
@@ -1009,6 +1011,9 @@ struct Ctl {
     unsigned op_n[O_DONE];
     unsigned long long item_ticks[O_DONE];  // op start → the last wave's items done
     unsigned long long first_ticks[O_DONE]; // op start → the first wave's items done
+    int fsz;                                // diagnostics: the running step's frontier size
+    unsigned long long hist_t[12];          //              sweep / BF ticks by frontier size (≤16, 64, 256, 1k, 4k, more)
+    unsigned hist_n[12];
 };
 __shared__ Ctl c_;
 
@@ -1051,7 +1056,20 @@ __device__ __forceinline__ void phase_end(const CellArgs& A) {
     }
 }
 
+__device__ __forceinline__ void control_body(const CellArgs& A, int N);
 __device__ __forceinline__ void control(const CellArgs& A, int N) {
+    Ctl& c = c_;
+    if (c.op == O_SWEEP || c.op == O_BF) {
+        const int f = c.fsz;
+        const int b = f <= 16 ? 0 : f <= 64 ? 1 : f <= 256 ? 2 : f <= 1024 ? 3 : f <= 4096 ? 4 : 5;
+        const int h = (c.op == O_BF ? 6 : 0) + b;
+        c.hist_t[h] += __builtin_amdgcn_s_memrealtime() - c.t_op;
+        ++c.hist_n[h];
+    }
+    control_body(A, N);
+    c.fsz = c.src < 2 ? total_any(c.src) : N;
+}
+__device__ __forceinline__ void control_body(const CellArgs& A, int N) {
     Ctl& c = c_;
     s_.next = 0;   // the next step's item dispenser (read after the barrier that follows)
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -1370,6 +1388,10 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
             o.cls_ticks[i] = (&cls_t_[0][0])[i];
             o.cls_n[i] = (&cls_n_[0][0])[i];
         }
+        for (int i = 0; i < 12; ++i) {
+            o.hist_t[i] = c.hist_t[i];
+            o.hist_n[i] = c.hist_n[i];
+        }
         A.out[blockIdx.x] = o;
     }
 }
@@ -1392,14 +1414,14 @@ __global__ void k_cell_pack(CellArgs A, int* bad) {
         const long long pb = A.first[x0];
         CellPos c;
         const bool dead = q.cost >= DEAD_SCALED;
-        const long long cu = dead ? 0 : q.cost / A.mult;
+        const long long cs = dead ? 0 : q.cost;   // scaled: the decode needs no multiply
         const long long hl = q.head - x0, rr = q.rev - pb;
-        if (q.ucap > CELL_MAX_CAP || q.rcap > CELL_MAX_CAP || cu > CELL_MAX_COST || cu < -CELL_MAX_COST ||
+        if (q.ucap > CELL_MAX_CAP || q.rcap > CELL_MAX_CAP || cs > CELL_MAX_COST || cs < -CELL_MAX_COST ||
             hl >= (1LL << CELL_HEAD_BITS) || rr < 0 || rr >= CELL_MAX_POS)
             atomicOr(bad, 1);
         c.rcap = (int)q.rcap;
         c.ucap = (int)q.ucap;
-        c.cost = dead ? CELL_DEAD : (int)cu;
+        c.cost = dead ? CELL_DEAD : (int)cs;
         c.hr = (unsigned)hl | ((unsigned)rr << CELL_HEAD_BITS);
         A.cp[p] = c;
     }

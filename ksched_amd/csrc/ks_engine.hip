@@ -3546,10 +3546,16 @@ void Engine::set_cells(const int64_t* off, size_t k) {
 
 // The cell solver runs when every cell (the ks_batch partition, else the whole
 // graph) fits one workgroup's LDS and ks_opts.cell_nodes allows it. Sizes are node
-// slots as the build lays them out (the current build's, or the next one's).
+// slots as the build lays them out (the current build's, or the next one's). By
+// default a lone graph takes it only up to kCellSingleNodes: one workgroup is one
+// CU's VALU, and above that size the multi-kernel engine over the whole chip solves
+// a single graph sooner (config 2: ~21 ms vs ~37 ms); a partition's cells run side
+// by side on separate CUs, so they take it up to the LDS limit.
+constexpr int64_t kCellSingleNodes = 4096;
 static bool want_cells(const EngineImpl& s) {
     if (s.opts.cell_nodes < 0 || s.cell_refused) return false;
-    const int64_t lim = std::min<int64_t>(cell_max_nodes(), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
+    int64_t lim = std::min<int64_t>(cell_max_nodes(), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
+    if (s.opts.cell_nodes == 0 && s.cell_off.size() < 2) lim = std::min(lim, kCellSingleNodes);
     const int64_t ncap =
         s.csr_valid ? s.ncap : s.nslots + (s.incremental ? std::max<int64_t>(64, s.nslots / 16) : 0);
     if (ncap <= 0) return false;
@@ -4444,6 +4450,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                     if (o.cls_n[8 * s + c])
                         std::fprintf(stderr, " c%d %u x %.2f us", c, o.cls_n[8 * s + c],
                                      o.cls_ticks[8 * s + c] / 100.0 / o.cls_n[8 * s + c]);
+            }
+            static const char* const sz[6] = {"<=16", "<=64", "<=256", "<=1k", "<=4k", ">4k"};
+            for (int h = 0; h < 12; ++h) {
+                if (h % 6 == 0) std::fprintf(stderr, "\n  %s by frontier:", h ? "bf" : "sweep");
+                if (o.hist_n[h])
+                    std::fprintf(stderr, " %s %u x %.2f us", sz[h % 6], o.hist_n[h], o.hist_t[h] / 100.0 / o.hist_n[h]);
             }
             std::fprintf(stderr, "\n");
         }

@@ -24,13 +24,17 @@ def load_known_answers():
         return json.load(f)
 
 
+CELL_ANY = 1 << 16   # ks_opts.cell_nodes above the LDS limit: the cell solver for whatever fits
+
+
 @pytest.fixture(scope="session")
 def ctx():
     """One HIP solver context shared by the GPU tests (one process on the box).
-    Default options: graphs up to the cell solver's size run in one workgroup
-    (ks_cell.hip), larger ones on the multi-kernel engine."""
+    cell_nodes = CELL_ANY: every graph the cell solver's LDS holds (config-2 size)
+    runs in one workgroup (ks_cell.hip), larger ones on the multi-kernel engine (by
+    default a lone graph takes the cell solver only up to 4,096 nodes)."""
     from ksched_amd import native
-    c = native.Context(0)
+    c = native.Context(0, cell_nodes=CELL_ANY)
     yield c
     c.close()
 

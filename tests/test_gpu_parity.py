@@ -4,7 +4,7 @@ capacity and conservation; task mappings validated (SURVEY §7 hard part 5)."""
 import numpy as np
 import pytest
 
-from conftest import load_goldens, load_known_answers
+from conftest import CELL_ANY, load_goldens, load_known_answers
 from graphs import graph_from_lists, random_graphs
 from ksched_amd import gen, native
 from oracle import ko
@@ -341,9 +341,7 @@ def test_failed_certificate_is_recovered(fault, path):
     Either way the solve returns the oracle's cost, the flow re-verified, and
     fault 2 always needs (and counts) a recovery — on the engine and inside the
     cell solver's workgroups (its recovery mode: refinement, else one ε = 1 phase)."""
-    opts = {"fault_inject": fault}
-    if path == "engine":
-        opts["cell_nodes"] = -1
+    opts = {"fault_inject": fault, "cell_nodes": -1 if path == "engine" else CELL_ANY}
     if fault == 1:
         opts["price_refine"] = 0
     with native.Context(0, **opts) as c2:

@@ -41,7 +41,7 @@ def main():
     for e in sel:
         g = graph_of(e)
         row = {"family": e["family"], "params": e["params"], "seed": e["seed"], "n": g.n, "gold": e["cost"]}
-        for name, opts in (("cell", {"log_cycles": args.log, **json.loads(args.opts)}), ("engine", {"cell_nodes": -1})):
+        for name, opts in (("cell", {"log_cycles": args.log, "cell_nodes": 1 << 16, **json.loads(args.opts)}), ("engine", {"cell_nodes": -1})):
             if name == "engine" and not args.engine:
                 continue
             ctx = native.Context(0, **opts)
