@@ -95,8 +95,9 @@ typedef struct ks_opts {
     int32_t  price_refine;     /* certify optimality early by price refinement (1)      */
     int32_t  gu_interval;      /* sweeps between global price updates (default 24)      */
     int32_t  warm_start;       /* 1: re-solve from the previous flow and prices after
-                                  ks_apply_deltas; 0 (default): every solve from
-                                  scratch (faster on config 4)      */
+                                  ks_apply_deltas (the first phase saturates only the
+                                  arcs violating its ε); 2: every phase does; 0
+                                  (default): every solve from scratch  */
     /* solver tuning; 0 selects the library default given in brackets.
        None of these changes the result — only how fast it is reached. */
     int32_t  walk_slack;       /* a phase's tail walkers take residual arcs of reduced cost
@@ -144,7 +145,11 @@ typedef struct ks_opts {
                                   to what its LDS holds (13,1xx), a lone graph up to 4,096
                                   (larger ones solve sooner on the whole chip)]; < 0:
                                   always the multi-kernel engine                          */
-    int32_t  reserved[3];
+    int32_t  warm_shift;       /* warm start: a node whose flow-carrying out-arc got dearer
+                                  since the last solve (ksched's ageing of unscheduled
+                                  arcs) is priced down by the rise, so that arc keeps its
+                                  reduced cost [0: on]; < 0 off                          */
+    int32_t  reserved[2];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */

@@ -102,7 +102,7 @@ struct CellArgs {
     long long mult;          // cost scaling (n + 1)
     long long eps_start;     // ε before the first phase's division by α
     long long sat_thr0;      // the first phase saturates arcs below −sat_thr0 (warm start), else 0
-    int warm;
+    int warm;                // 1: warm start (the first phase saturates only violations); 2: every phase
     int alpha;
     int pr_div;              // price refinement once ε·pr_div < mult
     int use_pr;

@@ -1023,7 +1023,7 @@ __device__ __forceinline__ int total_any(int src) { return total_of(src); }
 __device__ __forceinline__ void begin_phase(const CellArgs& A) {
     Ctl& c = c_;
     ++c.phases;
-    c.thr = (c.phases == 1 && A.warm) ? A.sat_thr0 : (c.pr_failed ? c.eps_ph : 0LL);
+    c.thr = (c.phases == 1 && A.warm) ? A.sat_thr0 : ((c.pr_failed || A.warm >= 2) ? c.eps_ph : 0LL);
     c.pr_failed = 0;
     const bool last = c.eps_ph / A.alpha < 1 || c.eps_ph <= 1 || (A.use_pr && c.eps_ph * A.pr_div < A.mult);
     c.early = last ? 0 : 1;

@@ -2534,6 +2534,20 @@ __global__ void k_restore_prices(int ncap, int n_prev, long long mult_prev, long
     }
 }
 
+// Warm start: a node whose flow-carrying out-arc got dearer by δ (cost units)
+// since the previous solve is priced down by δ·mult, so that arc keeps its
+// reduced cost (ks_store.hip k_arc_upserts records δ).
+__global__ void k_price_shift(int ncap, const unsigned long long* __restrict__ shift, const int* __restrict__ perm,
+                              long long mult, long long* __restrict__ nd) {
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK) {
+        const unsigned long long d = shift[v];
+        if (!d) continue;
+        const int x = perm[v];
+        nd[ni(x)] -= (long long)d * mult;
+        nd[ni(x) + 2] -= (long long)d * mult;
+    }
+}
+
 // Nodes created since the previous solve (fresh[v] = 1) get the lowest price
 // at which none of their residual out-arcs has a negative reduced cost.
 __global__ void k_fresh_prices(int ncap, const unsigned char* __restrict__ fresh, const int* __restrict__ perm, DG g) {
@@ -2772,6 +2786,7 @@ struct EngineImpl {
     int64_t nslots = 0;       // slots in use (max id)
     DBuf<long long> n_supply;
     DBuf<unsigned char> n_type, n_alive, n_fresh;
+    DBuf<unsigned long long> n_cshift;   // per slot: cost rise on a flow-carrying out-arc (warm start)
     DBuf<int> n_lastrm;
     DBuf<int> n_hint;         // per slot: segment capacity of the last build
     DBuf<unsigned char> n_grow;
@@ -2883,7 +2898,7 @@ struct EngineImpl {
             (void)hipSetDevice(device);
             (void)hipStreamSynchronize(stream);
         }
-        n_supply.release(); n_type.release(); n_alive.release(); n_fresh.release(); n_lastrm.release();
+        n_supply.release(); n_type.release(); n_alive.release(); n_fresh.release(); n_cshift.release(); n_lastrm.release();
         n_hint.release(); n_grow.release(); n_bind.release(); a_type.release(); sched_i.release(); sched_u.release();
         sched_b.release(); sched_d.release();
         a_src.release(); a_dst.release(); fwd.release(); free_stack.release(); a_low.release(); a_cap.release();
@@ -2930,6 +2945,7 @@ struct EngineImpl {
         d.n_type = n_type.p;
         d.n_alive = n_alive.p;
         d.n_fresh = n_fresh.p;
+        d.n_cshift = n_cshift.p;
         d.n_lastrm = n_lastrm.p;
         d.n_grow = n_grow.p;
         d.n_bind = n_bind.p;
@@ -3094,6 +3110,7 @@ static int ensure_nodes(EngineImpl& s, int64_t need, std::string& err) {
     KS_CHECK(s.n_type.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_alive.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_fresh.grow(cap, s.nstore, 0, st));
+    KS_CHECK(s.n_cshift.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_lastrm.grow(cap, s.nstore, 0xff, st));
     KS_CHECK(s.n_hint.grow(cap, s.nstore, 0, st));
     KS_CHECK(s.n_grow.grow(cap, s.nstore, 0, st));
@@ -3190,6 +3207,7 @@ int Engine::load(int64_t nslots, const int64_t* supply, const uint8_t* type, con
     KS_CHECK(hipMemsetAsync(s.n_supply.p, 0, s.nstore * sizeof(long long), st));
     KS_CHECK(hipMemsetAsync(s.n_type.p, 0, s.nstore, st));
     KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
+    KS_CHECK(hipMemsetAsync(s.n_cshift.p, 0, s.nstore * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.n_hint.p, 0, s.nstore * sizeof(int), st));
     KS_CHECK(hipMemsetAsync(s.n_grow.p, 0, s.nstore, st));
     KS_CHECK(hipMemsetAsync(s.n_bind.p, 0, s.nstore * sizeof(unsigned long long), st));
@@ -4357,6 +4375,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // the arcs that violate it
     long long warm_thr = 0;
     if (use_warm) {
+        if (o.warm_shift >= 0)
+            hipLaunchKernelGGL(k_price_shift, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
+                               (const unsigned long long*)s.n_cshift.p, (const int*)s.perm.p, mult, s.nd.p);
         hipLaunchKernelGGL(k_fresh_prices, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
                            (const unsigned char*)s.n_fresh.p, (const int*)s.perm.p, g);
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
@@ -4395,7 +4416,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.mult = mult;
         a.eps_start = eps_cells;
         a.sat_thr0 = warm_thr;
-        a.warm = use_warm ? 1 : 0;
+        a.warm = use_warm ? (o.warm_start >= 2 ? 2 : 1) : 0;
         a.alpha = alpha;
         a.pr_div = (int)pr_div;
         a.use_pr = use_pr ? 1 : 0;
@@ -4495,7 +4516,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // saturating only the arcs that violate the new ε (rc < −ε) is a valid start
         // (push-relabel at ε needs an ε-optimal pseudoflow, not a 0-optimal one) and
         // disturbs far less than saturating every negative arc.
-        const long long sat_thr = phases == 1 && use_warm ? warm_thr : (pr_failed ? eps : 0LL);
+        // warm_start 2: every phase of a warm solve saturates only the arcs that
+        // violate its ε (the previous optimum's arcs in [−1, 0) stay as they are)
+        const long long sat_thr =
+            phases == 1 && use_warm ? warm_thr : ((pr_failed || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
         pr_failed = false;
         const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
         // walk slack > 1 only while a finer phase or price refinement still follows
@@ -4667,6 +4691,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.cell_ticks_max = cticks_max;
     res.cell_ticks_sum = cticks_sum;
     res.status = status;
+    KS_CHECK(hipMemsetAsync(s.n_cshift.p, 0, s.nstore * sizeof(unsigned long long), st));
     if (status == KS_OK) {
         KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
         KS_CHECK(hipStreamSynchronize(st));

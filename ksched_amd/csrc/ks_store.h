@@ -61,6 +61,8 @@ struct StoreDev {
     unsigned char* n_type;
     unsigned char* n_alive;
     unsigned char* n_fresh;       // per slot: (re)created since the last solve (warm start)
+    unsigned long long* n_cshift; // per slot: the largest cost increase on one of its flow-carrying
+                                  // out-arcs since the last solve (warm start: its price drops by it)
     int* n_lastrm;                // per slot: last REMOVE position of the current apply, −1
     unsigned char* n_grow;        // per slot: an insert did not fit its segment (next build doubles it)
     unsigned long long* n_bind;   // per slot: bound PU node id (task bindings), 0 = none

@@ -254,7 +254,7 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
         }
         const int sl = (int)x.src - 1, dl = (int)x.dst - 1;
         const long long low = (long long)x.low, cap = (long long)x.cap, u = cap - low;
-        const long long low_old = d.a_low[s];
+        const long long low_old = d.a_low[s], cost_old = d.a_cost[s];
         d.a_src[s] = sl;
         d.a_dst[s] = dl;
         d.a_low[s] = low;
@@ -283,6 +283,12 @@ __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k,
                 atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)back);
                 atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)(-back));
             }
+            // a cost rise on an arc that keeps its flow (ksched's ageing of the
+            // arcs to the unscheduled aggregators, graph_manager.go:462-475): the
+            // warm start lowers the tail's price by it, so the arc keeps its reduced
+            // cost and only the tail's other arcs lose that much slack
+            if (fn > 0 && x.cost > cost_old)
+                atomicMax(&d.n_cshift[sl], (unsigned long long)(x.cost - cost_old));
             atomicAdd(&d.ctl->updated, 1);
             continue;
         }

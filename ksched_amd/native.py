@@ -52,7 +52,8 @@ class KsOpts(C.Structure):
                 ("bf_margin", C.c_int32), ("two_hop", C.c_int32), ("log_cycles", C.c_int32),
                 ("fault_inject", C.c_int32), ("walk_passes", C.c_int32), ("tail_nodes", C.c_int32),
                 ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32), ("cell_nodes", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("warm_shift", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 class KsResult(C.Structure):
