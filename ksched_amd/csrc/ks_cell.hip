@@ -157,6 +157,14 @@ __device__ __forceinline__ Pos dec(const CellArgs& A, const K& k, int4 w) {
     return r;
 }
 __device__ __forceinline__ Pos ld_cp(const CellArgs& A, const K& k, int a) { return dec(A, k, ld_raw(A, a)); }
+// Pins a batch's loaded records in VGPRs at this point (one wait for the whole
+// batch): without it the compiler sinks a load into the branch of its only use,
+// where it gets its own s_waitcnt and the batch runs one load at a time.
+template <int N>
+__device__ __forceinline__ void pin(int4 (&q)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(q[i].x), "+v"(q[i].y), "+v"(q[i].z), "+v"(q[i].w));
+}
 __device__ __forceinline__ void st_rcap(const CellArgs& A, int a, long long v) { A.cp[a].rcap = (int)v; }
 
 __device__ __forceinline__ void seg(const CellArgs& A, int x, int& b0, int& b1) {
@@ -409,6 +417,7 @@ __device__ __forceinline__ void sweep_wave(const CellArgs& A, K& k, int nb, int 
             const int a = base + 64 * u + ln;
             qr[u] = ld_raw(A, a < en ? a : b0);
         }
+        pin(qr);
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const Pos Q = dec(A, k, qr[u]);
@@ -465,6 +474,7 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
         int4 qr[UC];
 #pragma unroll
         for (int u = 0; u < UC; ++u) qr[u] = ld_raw(A, a0 + u < en ? a0 + u : b0);
+        pin(qr);
         long long cr[UC];
         int adm[UC], my = 0;
 #pragma unroll
@@ -538,15 +548,16 @@ template <int W, bool PR>
 __device__ __forceinline__ void bf_node(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const int dv = dst(k)[v - k.x0];
     if (!PR && dv >= DINF) return;
+    const int me = W == 64 ? lane() : (int)threadIdx.x;
     const long long pv = prc()[v - k.x0];
     int b0, en;
     seg(A, v, b0, en);
-    const int me = W == 64 ? lane() : (int)threadIdx.x;
     for (int base = b0 + me; base < en; base += W * UC) {
         int4 qr[UC];
 #pragma unroll
         for (int u = 0; u < UC; ++u)
             qr[u] = ld_raw(A, base + W * u < en ? base + W * u : base);
+        pin(qr);
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const Pos Q = dec(A, k, qr[u]);
@@ -574,6 +585,7 @@ __device__ __forceinline__ void sat_node(const CellArgs& A, K& k, int v, long lo
 #pragma unroll
         for (int u = 0; u < UC; ++u)
             qr[u] = ld_raw(A, base + W * u < en ? base + W * u : base);
+        pin(qr);
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const Pos Q = dec(A, k, qr[u]);
@@ -623,6 +635,7 @@ __device__ __forceinline__ void leaf_load(const CellArgs& A, const K& k, int lig
         const int a = b0[u] + lig;
         qr[u] = ld_raw(A, a < en[u] ? a : 0);
     }
+    pin(qr);
 }
 
 template <int G, int U>
@@ -744,6 +757,7 @@ __device__ __forceinline__ int thr_load(const CellArgs& A, const K& k, int v, in
     const int cnt = v >= 0 ? en - b0 : 0;
 #pragma unroll
     for (int i = 0; i < MAXP; ++i) qr[i] = ld_raw(A, i < cnt ? b0 + i : 0);
+    pin(qr);
     return cnt;
 }
 

@@ -4,6 +4,7 @@ cost and flow against the CPU oracle on the equivalent full graphs."""
 import numpy as np
 import pytest
 
+from conftest import CELL_ANY
 from graphs import same_graph
 from test_gpu_parity import check_mapping, flows_by_arc
 from ksched_amd import churn, gen, native
@@ -12,14 +13,18 @@ from oracle import ko
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("warm", [0, 1])
-def test_incremental_rounds_match_full_resolve(warm):
+@pytest.mark.parametrize("warm,shift,path", [(0, 0, "engine"), (1, 0, "engine"), (2, 0, "engine"),
+                                              (2, -1, "engine"), (0, 0, "cell"), (2, 0, "cell")])
+def test_incremental_rounds_match_full_resolve(warm, shift, path):
     """Config 4 at config-2 scale: pins, completions, arrivals, ageing and
     capacity refresh as one delta stream per round; the device result after
     applying the deltas equals the oracle on the cell's full graph, re-solved
-    from scratch (warm_start 0) or from the previous flow and prices (1)."""
+    from scratch (warm_start 0) or from the previous flow and prices (1: the
+    first phase saturates only violations, 2: every phase does; warm_shift −1
+    turns off the price shift that absorbs the ageing), on the multi-kernel
+    engine and on the cell solver."""
     cell = churn.Cell(10_000, 1_000, 25, 100, 2)
-    ctx = native.Context(0, warm_start=warm)
+    ctx = native.Context(0, warm_start=warm, warm_shift=shift, cell_nodes=-1 if path == "engine" else CELL_ANY)
     ctx.load_graph(cell.graph())
     r = ctx.solve()
     mp = ctx.task_mapping()
@@ -31,7 +36,8 @@ def test_incremental_rounds_match_full_resolve(warm):
         st, cost, flow, _ = ko.cost_scaling(g)
         assert st == 0
         assert (r.cost, r.flow) == (cost, flow), f"round {rnd + 1}"
-        assert r.raw["warm_started"] == warm
+        assert r.raw["warm_started"] == (1 if warm else 0)
+        assert r.raw["solver"] == (1 if path == "cell" else 0) and r.raw["recoveries"] == 0
         fl = flows_by_arc(ctx, g)
         vst, vcost, _ = ko.verify(g, fl)
         assert vst == 0 and vcost == cost
