@@ -60,7 +60,7 @@ def pmc_file(workload: str):
 KINDS = {
     "k_sweep": ("sweep_launches", "ms_sweep_kernels", ("arc_scans", "node_visits", "pushes")),
     "k_bf_round": ("gu_launches", "ms_gu_kernels", ("gu_arc_scans",)),
-    "k_fs_round": ("fs_launches", "ms_fs_kernels", ()),
+    "k_fs_round": ("fs_launches", "ms_fs_kernels", ("fs_arc_scans",)),
     "k_cell": (None, "ms_cell_kernel", ("arc_scans", "node_visits", "pushes", "gu_arc_scans")),
 }
 
@@ -83,7 +83,7 @@ def roofline_of(results, workload: str):
     counters' units, divided by the HIP-event-timed duration of that kernel's
     launches (each kind's span brackets exactly its own kernels, ks_result ABI 3).
     For k_bf_round the 44 B the relaxation actually reads is reported beside it;
-    the forward search (k_fs_round) has no unit counter and is reported by time.
+    the forward search (k_fs_round) counts the residual out-arcs it examines.
     The cell solver (k_cell, one launch per solve) does all four kinds of work
     in one kernel: its units are all of them. ``traffic`` (PMC bytes per launch)
     cannot be collected inside this run (rocprofv3 --pmc is its own pass): it is

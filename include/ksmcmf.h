@@ -228,7 +228,8 @@ typedef struct ks_result {
     double   ms_cell_kernel;   /* event-timed duration of the cell-solver launches (ms) */
     uint64_t cell_ticks_max;   /* slowest cell's in-kernel solve time (100 MHz ticks)   */
     uint64_t cell_ticks_sum;   /* Σ over cells of their in-kernel solve times            */
-    uint64_t reserved2[4];
+    uint64_t fs_arc_scans;     /* residual out-arcs the forward tail searches examined    */
+    uint64_t reserved2[3];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

@@ -87,14 +87,15 @@ constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
 constexpr int CYC_SLOTS = 2;       // control snapshots / timing events rotate over two cycles
-constexpr int NCTR = 8;
+constexpr int NCTR = 9;
 constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
 constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-converging solve
 constexpr double kCellLimitS = 20.0;       // the cell solver's in-kernel wall-clock limit (every workgroup exits)
 
-enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7 };
+enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7,
+       C_FSSCAN = 8 };
 constexpr int AUG_KMAX = 4096;     // most excess nodes a tail's walkers start from (ks_opts.tail_nodes)
 constexpr int BX_CAP = 64;         // global updates with at most this many excess nodes are bounded
 // Forward tail update: a node's search key (in its record's dist slot) packs the
@@ -2215,6 +2216,14 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
     if (done) return;
     const int nhb = g.nhitems * HSPLIT;
     const int lane = lane_id();
+    long long scans = 0;   // residual out-arcs examined (the round's units, ks_result.fs_arc_scans)
+    auto count = [&]() {
+        scans = wave_sum(scans);
+        if (lane == 0 && scans) {
+            const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
+            atomicAdd(g.ctr + sh * NCTR + C_FSSCAN, (unsigned long long)scans);
+        }
+    };
     if ((int)blockIdx.x < nhb) {
         const HItem it = g.hitems[blockIdx.x / HSPLIT];
         if (!F.hub[it.hid]) return;
@@ -2225,8 +2234,10 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
             const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
             int w = -1;
             const int add = a < it.end ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            scans += a < it.end;
             fs_append(g, lout, add, w);
         }
+        count();
         return;
     }
     // listed nodes: one wave each, 64 arcs per pass (eight nodes per wave with eight
@@ -2247,9 +2258,11 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
             const int a = base + lane;
             int w = -1;
             const int add = a < b1 ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            scans += a < b1;
             fs_append(g, lout, add, w);
         }
     }
+    count();
 }
 
 // Apply the dual step of a converged search: p ← p − ε·(D − d_f) below D, and
@@ -4681,6 +4694,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.ms_phase[4] = ev_ms(s.ev[6], s.ev[7]);
     res.ms_phase[5] = 1e3 * wall_s();
     res.gu_arc_scans = tc[C_GUSCAN];
+    res.fs_arc_scans = tc[C_FSSCAN];
     res.sweep_launches = sweep_kernels;
     res.ms_sweep_kernels = ms_sw_k;
     res.gu_launches = bf_launches;
