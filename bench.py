@@ -618,6 +618,7 @@ def run_batch(args, D):
               "graphs": num, "tasks": T, "machines": M, "graphs_per_gpu": len(mine), "mode": args.batch_mode,
               "parallelism": f"graph sharding x{D.world}"}
     line = base_line(args, D, value, ms_per_step, config, step_ms=[round(x, 2) for x in step_ms],
+                     scaling="strong",   # a fixed 64 graphs shared by the ranks
                      roofline=roofline_of(results, "config5"), cpu_baseline=cpu, gather=gather, parity=parity,
                      latency=latency_stats(step_ms), cell_latency=extra_cells, solve=dict(results[-1].raw))
     if args.batch_mode == "abi":
