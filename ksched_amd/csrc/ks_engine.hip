@@ -215,7 +215,6 @@ struct DG {
     Front bf[3];   // Bellman-Ford frontiers
     Ctl* ctl;
     unsigned long long* ctr;
-    unsigned long long* stamps;   // diagnostic builds (-DKS_STAMPS): per launch [first start, last end|kind]
 };
 
 // Node records: p0, dist, p1 and the node's segment bounds (first[x], first[x+1]
@@ -1004,7 +1003,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
 // per pass (two per thread, all loads issued together), the excess distributed
 // by one block-wide scan. A rack (≈ 440 arcs) is one pass — with one wave per
 // node it took two dependent batches, and the chunked node was the last block
-// of almost every sweep (tools/stamps.py).
+// of almost every sweep (round 3's per-launch block stamps).
 __device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, int x, long long e, long long px,
                                    int b0, int en, long long* __restrict__ PN, const long long* __restrict__ P,
                                    long long eps, Pend& pd, int& out, Cnt& c) {
@@ -1188,26 +1187,6 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
     }
 }
 
-#ifdef KS_STAMPS
-constexpr int STAMP_W = 11;
-// Diagnostic: per launch, the earliest block start and the latest end of a block
-// that did work, tagged with that block's kind (1 hub chunk, 2 chunked node,
-// 3 + c window class c).
-__device__ __forceinline__ void stamp(const DG& g, int id, unsigned long long t0, int busy, int kind,
-                                      unsigned long long work) {
-    const int any = __syncthreads_or(busy);
-    work = wave_sum((long long)work);
-    if (lane_id() == 0 && work && g.stamps && id >= 0 && id < 8192) atomicAdd(&g.stamps[STAMP_W * id + 10], work);
-    if (threadIdx.x == 0 && any && g.stamps && id >= 0 && id < 8192) {
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        unsigned long long* r = g.stamps + (size_t)STAMP_W * id;
-        atomicMin(&r[0], t0);
-        atomicMax(&r[1], (t1 << 4) | (unsigned long long)kind);
-        atomicMax(&r[2], t0);                       // latest start of a working block
-        atomicMax(&r[2 + kind], t1 - t0);           // longest block of this kind
-    }
-}
-#endif
 
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     if (blockIdx.x == 0)
@@ -1221,10 +1200,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         c_done = g.ctl->bf_done;
         c_act = pos == 0 ? g.ctl->apply_act : g.ctl->sweep_act[pos - 1];
     };
-#ifdef KS_STAMPS
-    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-    int kind = 0;
-#endif
     const Front F = g.sf[seq % 3], N = g.sf[(seq + 1) % 3];
     const long long eps = g.ctl->eps;
     const long long* P = (pos & 1) ? g.p1 : g.p0;
@@ -1241,9 +1216,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(px), "v"(E));
         if (c_done && c_act && fl) {
             hub_chunk(g, F, N, it, px, E, P, PN, eps, pd, out, c);
-#ifdef KS_STAMPS
-            kind = 1;
-#endif
         }
     } else if ((int)blockIdx.x >= g.nhitems + g.sw_clsb) {
         // chunked class: one workgroup per node (a wave per node made the chunked
@@ -1271,9 +1243,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             __syncthreads();
             if (s_go) {
                 node_discharge_blk(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
-#ifdef KS_STAMPS
-                kind = 2;
-#endif
             }
         }
     } else {
@@ -1298,9 +1267,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         for (int j = 0; j < WPW; ++j) {
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
-#ifdef KS_STAMPS
-            kind = max(kind, 3 + class_of_window(g, w));
-#endif
             switch (class_of_window(g, w)) {
                 case 0: sweep_win<0>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
                 case 1: sweep_win<1>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
@@ -1312,16 +1278,6 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     }
     if (__any(out) && lane_id() == 0) g.ctl->sweep_act[pos] = 1;
     flush_counters(g, c);
-#ifdef KS_STAMPS
-    {   // the block's kind = the max over its waves
-        __shared__ int sk[WPB];
-        if (lane_id() == 0) sk[threadIdx.x >> 6] = kind;
-        __syncthreads();
-        int k2 = 0;
-        for (int i = 0; i < WPB; ++i) k2 = max(k2, sk[i]);
-        stamp(g, seq & 4095, ts0, kind > 0, k2, (unsigned long long)c.visit);
-    }
-#endif
 }
 
 // ================================================ Bellman-Ford (GU and PR) ===
@@ -1536,10 +1492,6 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         done = g.ctl->bf_done;
         any = g.ctl->bfa[seq % 3];
     };
-#ifdef KS_STAMPS
-    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-    int kind = (int)blockIdx.x < g.nhitems * HSPLIT ? 1 : 0;
-#endif
     const long long eps = g.ctl->eps;
     // bounded update (tail): offers at or above the listed excess nodes' largest
     // tentative distance are dropped (that bound only falls, so a stale copy is safe)
@@ -1614,14 +1566,8 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
                 bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
-#ifdef KS_STAMPS
-                kind = max(kind, 2);
-#endif
                 continue;
             }
-#ifdef KS_STAMPS
-            kind = max(kind, 3 + class_of_window(g, w));
-#endif
             switch (class_of_window(g, w)) {
                 case 0: bf_win<0, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
                 case 1: bf_win<1, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
@@ -1664,15 +1610,6 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         }
     }
     scans = wave_sum(scans);
-#ifdef KS_STAMPS
-    {
-        __shared__ int sk[WPB];
-        if (lane_id() == 0) sk[threadIdx.x >> 6] = kind;
-        __syncthreads();
-        for (int i = 0; i < WPB; ++i) kind = max(kind, sk[i]);
-    }
-    stamp(g, 4096 + (seq & 4095), ts0, scans > 0, kind, (unsigned long long)(lane_id() == 0 ? scans : 0));
-#endif
     if (lane_id() == 0 && scans) {
         const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
         atomicAdd(g.ctr + sh * NCTR + C_GUSCAN, (unsigned long long)scans);
@@ -2866,7 +2803,6 @@ struct EngineImpl {
     DBuf<int> bx;                      // excess nodes of the running update (distance bound)
     DBuf<int> fl, fdef;                // forward tail update: frontier lists, traced deficits
     DBuf<long long> aug_req;           // per hub claim counter (k_aug_hub)
-    DBuf<unsigned long long> stamps;   // KS_STAMPS diagnostic builds only
     DBuf<Ctl> ctl;
     Ctl* h_ctl = nullptr;        // pinned host mirror
     long long* h_scr = nullptr;  // pinned scratch: [0] eps, [1] max |cost|
@@ -3058,7 +2994,6 @@ struct EngineImpl {
         }
         g.ctl = ctl.p;
         g.ctr = ctr.p;
-        g.stamps = stamps.n > 1 ? stamps.p : nullptr;
         return g;
     }
     int window_grid() const { return nhitems + std::max(1, (wbeg[NGC] + WPB - 1) / WPB); }
@@ -4067,16 +4002,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     KS_CHECK(hipEventRecord(s.ev[1], st));
 
     // ------------------------------------------------------------ phases ---
-#ifdef KS_STAMPS
-    const char* stamp_path = std::getenv("KS_STAMPS_OUT");   // diagnostic builds only
-    if (stamp_path) {
-        KS_CHECK(s.stamps.ensure(STAMP_W * 8192));
-        std::vector<unsigned long long> init(STAMP_W * 8192, 0);
-        for (int i = 0; i < 8192; ++i) init[STAMP_W * i] = ~0ULL;
-        KS_CHECK(hipMemcpyAsync(s.stamps.p, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
-        KS_CHECK(hipStreamSynchronize(st));
-    }
-#endif
     // Tuning comes from ks_opts only (0 = default; include/ksmcmf.h): nothing in
     // the environment changes the algorithm.
     const ks_opts& o = s.opts;
@@ -4691,22 +4616,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         std::fprintf(stderr, "solve tail walks to a deficit %llu, hops %llu, recoveries %d\n", tc[C_AUGWALK],
                      tc[C_AUGHOP], res.recoveries);
 
-#ifdef KS_STAMPS
-    if (stamp_path && s.stamps.n > 1) {
-        std::vector<unsigned long long> hs(STAMP_W * 8192);
-        KS_CHECK(hipMemcpy(hs.data(), s.stamps.p, hs.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(stamp_path, "a")) {
-            for (int i = 0; i < 8192; ++i) {
-                const unsigned long long* r = &hs[STAMP_W * i];
-                if (!r[1]) continue;
-                std::fprintf(f, "%d %llu %llu %llu %llu", i, r[0], r[1] >> 4, r[1] & 15, r[2] - r[0]);
-                for (int k = 3; k < STAMP_W; ++k) std::fprintf(f, " %llu", r[k]);
-                std::fprintf(f, "\n");
-            }
-            std::fclose(f);
-        }
-    }
-#endif
     res.total_cost = tot_cost;
     res.flow_value = tot_flow;
     res.phases = phases;

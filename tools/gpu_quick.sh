@@ -1,5 +1,4 @@
 #!/bin/bash
-# Quick GPU iteration: parity tests, config-3 bench (no CPU baseline), stamps diagnostic.
 # Usage: gpu_quick.sh TAG [pytest -k expr]
 set -o pipefail
 TAG=${1:-quick}
@@ -13,6 +12,3 @@ tail -1 "$OUT/pytest.log"
 timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --cpu-baseline off > "$OUT/bench.json" 2> "$OUT/bench.err" \
     || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
 python -c "import json,sys; d=json.load(open('$OUT/bench.json')); print('config3 ms/step', d['ms_per_step'], 'steps', d['step_ms'], 'cost', d['parity']['gpu_costs'])"
-timeout -k 10 200 python -u tools/stamps.py config3 --solves 2 --out "$OUT/stamps.txt" > "$OUT/stamps.log" 2>&1 \
-    || { echo "stamps failed"; tail -30 "$OUT/stamps.log"; exit 1; }
-cat "$OUT/stamps.log"

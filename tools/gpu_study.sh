@@ -1,5 +1,4 @@
 #!/bin/bash
-# Tail study: kernel trace with per-cycle breakdown, stamps (work per launch), device tail dump.
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/study
@@ -8,8 +7,6 @@ timeout -k 10 200 rocprofv3 --kernel-trace -f csv -d $OUT/kt -o run -- python -u
 python tools/kernel_trace.py $OUT/kt --seq --cycles > $OUT/kt.txt
 rm -rf $OUT/kt
 head -24 $OUT/kt.txt
-timeout -k 10 200 python -u tools/stamps.py config3 --solves 2 --out $OUT/stamps.txt > $OUT/stamps.log 2>&1 || { echo stamps failed; tail $OUT/stamps.log; exit 1; }
-rm -f $OUT/stamps.txt
 gcc -O2 -o /tmp/tail_dump tools/proto/tail_dump.c
 KS_LIB_VARIANT=dump KS_DUMP=/tmp/tail.dump timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 \
     --cpu-baseline off > $OUT/dump_bench.json 2> $OUT/dump_bench.err || exit 1
