@@ -13,14 +13,21 @@
 //   LDS       the cell's prices (int64) and Bellman-Ford distances (int32,
 //             saturating at 2^30: any cap keeps the triangle inequality the
 //             update needs) live in LDS, 12 B per node, so the random gather of
-//             a relaxation or an arc scan is an LDS read; only the 32-B
-//             residual positions (streamed along each node's segment) and the
-//             excess words come from L2.
+//             a relaxation or an arc scan is an LDS read; only the 16-B compact
+//             residual positions (CellPos, streamed along each node's segment),
+//             the segment table and the excess words come from L2.
 //   frontier  per-class lists: a node enters the next frontier once, through a
 //             test-and-set in an LDS bitmap, appended at its class's slice of a
-//             list buffer in HBM; the next step takes lane groups of 4…64 lanes
-//             per node (classes ≤ 64 positions), one wave per node (≤ 512) or
-//             the whole workgroup (the cluster aggregator).
+//             list buffer in HBM. Waves take items from an LDS counter, the
+//             costliest classes first: the whole workgroup per node above 512
+//             positions (the cluster aggregator, the sink), one wave per node
+//             (≤ 512), a 16- or 32-lane group per node (≤ 32: machines), one
+//             thread per node (≤ 8: tasks, PUs — a bitmask of the positions that
+//             need a push / relaxation / saturation, then only those).
+//   VALU      a solve is VALU-bound on its CU (PMC: ~7.5e7 VALU instructions over
+//             ~1.1e8 cycles); batched record loads are issued unconditionally and
+//             pinned (a load in a lane-conditional branch waits there), lane-group
+//             scans are DPP with the group's last lane as leader.
 //   snapshot  sweeps read one price array and defer relabels to the end of the
 //             sweep (a pending list applied after the barrier) — the snapshot
 //             semantics of the engine's double-buffered prices (at
