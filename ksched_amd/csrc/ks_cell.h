@@ -112,6 +112,7 @@ struct CellArgs {
     int mode;                // 0: solve from the state in place; 1: certificate recovery at ε = 1
     int max_nodes;           // largest cell (sizes the LDS)
     unsigned long long timeout_ticks;   // a cell's solve gives up after this many 100 MHz ticks
+    int diag;                // per-item / per-class timing for the cycle log (ks_opts.log_cycles)
     const int* bad;          // set by k_cell_pack: a value the compact record cannot hold
 };
 

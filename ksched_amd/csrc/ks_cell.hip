@@ -945,12 +945,12 @@ __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, l
     for (int j = 0; j < n6; ++j) {
         const int v = node_at(A, src, 6, j);
         __syncthreads();   // the previous node's pushes and marks are in
-        const unsigned long long h0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long h0 = A.diag ? __builtin_amdgcn_s_memrealtime() : 0;
         if (OP == OP_SWEEP) sweep_hub(A, k, nb, v, t);
         else if (OP == OP_BF) bf_node<CT, false>(A, k, nb, v, t);
         else if (OP == OP_PR) bf_node<CT, true>(A, k, nb, v, t);
         else sat_node<CT>(A, k, v, thr, t);
-        if (threadIdx.x == 0) {
+        if (A.diag && threadIdx.x == 0) {
             atomicAdd(&cls_t_[OP][6], __builtin_amdgcn_s_memrealtime() - h0);
             atomicAdd(&cls_n_[OP][6], 1u);
         }
@@ -971,7 +971,7 @@ __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, l
         if (lane() == 0) it0 = atomicAdd(&s_.next, 1);
         const int it = __builtin_amdgcn_readfirstlane(it0);
         if (it >= e0) break;
-        const unsigned long long i0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long i0 = A.diag ? __builtin_amdgcn_s_memrealtime() : 0;
         const int cl = it < e5 ? 5 : it < e4 ? 4 : it < e3 ? 3 : it < e2 ? 2 : it < e1 ? 1 : 0;
         if (it < e5) item<OP, 5>(A, k, src, nb, it, n5, thr, t);
         else if (it < e4) item<OP, 4>(A, k, src, nb, it - e5, n4, thr, t);
@@ -979,13 +979,13 @@ __device__ __forceinline__ void step(const CellArgs& A, K& k, int src, int nb, l
         else if (it < e2) item<OP, 2>(A, k, src, nb, it - e3, n2, thr, t);
         else if (it < e1) item<OP, 1>(A, k, src, nb, it - e2, n1, thr, t);
         else item<OP, 0>(A, k, src, nb, it - e1, n0, thr, t);
-        if (lane() == 0) {
+        if (A.diag && lane() == 0) {
             atomicAdd(&cls_t_[OP][cl], __builtin_amdgcn_s_memrealtime() - i0);
             atomicAdd(&cls_n_[OP][cl], 1u);
         }
     }
     flush(t);
-    if (lane() == 0) {   // when this wave's items were done (diagnostics: item span vs barrier tail)
+    if (A.diag && lane() == 0) {   // when this wave's items were done (diagnostics: item span vs barrier tail)
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         atomicMax(&t_items_, now);
         atomicMin(&t_first_, now);

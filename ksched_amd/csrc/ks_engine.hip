@@ -4398,6 +4398,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.mode = mode;
         a.max_nodes = s.cell_max;
         a.timeout_ticks = (unsigned long long)(kCellLimitS * 1e8);
+        a.diag = cycle_log ? 1 : 0;
         KS_CHECK(hipEventRecord(s.kev[2], st));
         KS_CHECK(cell_launch(a, s.cl_bad.p, st));
         KS_CHECK(hipEventRecord(s.kev[3], st));
