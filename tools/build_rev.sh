@@ -11,6 +11,10 @@ for f in $(git -C "$ROOT" ls-tree --name-only "$REV" ksched_amd/csrc/); do
 done
 git -C "$ROOT" show "$REV:include/ksmcmf.h" > "$T/include/ksmcmf.h"
 cd "$T/ksched_amd/csrc"
+SRCS=""
+for f in ks_engine.hip ks_cell.hip ks_store.hip ks_sched.hip ks_batch.hip ks_host.cpp; do
+    [ -f "$f" ] && SRCS="$SRCS $f"
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function -I"$T/include" \
-    ks_engine.hip ks_store.hip ks_sched.hip ks_batch.hip ks_host.cpp -ldl -o "$ROOT/ksched_amd/libksmcmf_$TAG.so"
+    $SRCS -ldl -o "$ROOT/ksched_amd/libksmcmf_$TAG.so"
 rm -rf "$T"
