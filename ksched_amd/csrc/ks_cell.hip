@@ -453,7 +453,7 @@ __device__ __forceinline__ void sweep_wave(const CellArgs& A, K& k, int nb, int 
         }
         if (rem == 0) break;
     }
-    minc = lane63_64(gs_min<64>(minc, ln));
+    if (rem > 0) minc = lane63_64(gs_min<64>(minc, ln));   // (rem is uniform: only a relabel needs it)
     if (ln == 63) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
@@ -513,7 +513,7 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
         rem -= tot < rem ? tot : rem;
         if (rem == 0) break;
     }
-    minc = blk_min(minc);
+    if (rem > 0) minc = blk_min(minc);   // (uniform over the workgroup)
     if (threadIdx.x == 0) {
         const long long pushed = e - rem;
         if (pushed) add_ex(A, v, -pushed);
@@ -692,7 +692,9 @@ __device__ __forceinline__ void sweep_leaf(const CellArgs& A, K& k, int nb, cons
                 minc = cr;
             }
         }
-        minc = gs_min<G>(minc, lig);                                // the last lane: the group minimum
+        // the group minimum (at the last lane) — only when some node of the wave
+        // keeps excess and relabels: a node that pushed it all does not need it
+        if (__ballot(act && lead && e[u] > incl)) minc = gs_min<G>(minc, lig);
         if (act && lead) {
             const long long rem = e[u] > incl ? e[u] - incl : 0;
             const long long pushed = e[u] - rem;
