@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 measurement: one bench line per headline workload (with its CPU
 # baseline legs), then the PMC + kernel-trace passes of each workload
-# (tools/gpu_pmc.sh). Usage: gpu_r04_final.sh TAG [bench|pmc|all]
+# (tools/gpu_pmc.sh). Usage: gpu_r04_final.sh TAG [bench|pmc|trace|all]
 set -o pipefail
 TAG=${1:-r04}
 OUT=gpurun_out/$TAG
@@ -26,9 +26,10 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
     bench config4 --workload incremental
     bench config5 --workload batch
 fi
-if [ "$WHAT" = pmc ] || [ "$WHAT" = all ]; then
+if [ "$WHAT" != bench ]; then
+    PASSES=all; [ "$WHAT" = trace ] && PASSES=trace
     for wl in config3 config2 config4 config5; do
-        bash tools/gpu_pmc.sh "${TAG}_pmc_$wl" "$wl" > "$OUT/pmc_$wl.log" 2>&1 \
+        bash tools/gpu_pmc.sh "${TAG}_pmc_$wl" "$wl" "$PASSES" > "$OUT/pmc_$wl.log" 2>&1 \
             || { echo "pmc $wl failed"; tail -20 "$OUT/pmc_$wl.log"; exit 1; }
         echo "pmc $wl ok"
     done
