@@ -113,6 +113,7 @@ struct CellArgs {
     int max_nodes;           // largest cell (sizes the LDS)
     unsigned long long timeout_ticks;   // a cell's solve gives up after this many 100 MHz ticks
     int diag;                // per-item / per-class timing for the cycle log (ks_opts.log_cycles)
+    int bound;               // 1: bounded global updates (ks_opts.bf_bound >= 0)
     const int* bad;          // set by k_cell_pack: a value the compact record cannot hold
 };
 

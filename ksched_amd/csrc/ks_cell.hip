@@ -51,6 +51,7 @@ constexpr long long DCAP = 1LL << 30;      // distances saturate here
 constexpr long long DNEG = -(1LL << 30);   // price refinement below this: treated as a negative cycle
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr size_t LDS_LIMIT = 163840;       // one workgroup may declare all 160 KiB on gfx950
+constexpr int BXC = 64;                    // updates with at most this many excess nodes are bounded
 
 enum { OP_SWEEP = 0, OP_BF = 1, OP_PR = 2, OP_SAT = 3 };
 enum { F_INFEAS = 1, F_NEG = 2 };
@@ -62,6 +63,9 @@ struct St {
     int flag;             // F_INFEAS | F_NEG
     int stop;             // the wall-clock limit was hit
     int next;             // the step's next item (waves take items dynamically)
+    int bnd;              // bounded update: offers at or above this distance are dropped (DINF: none)
+    int nbx;              // excess nodes listed by gu_init (more than BXC: the update is unbounded)
+    int bx[BXC];          // their local indices
     long long red[NW];
 };
 
@@ -81,6 +85,7 @@ struct K {
     long long eps;
     int eps_shift;        // log2 ε when ε is a power of two (the cell ladder's are), else −1
     int sp;               // sweep parity (pending-relabel buffer)
+    int bnd;              // s_.bnd at the step's start
 };
 
 // Work counters (ks_result units): counted per lane in registers, summed over the
@@ -542,6 +547,7 @@ __device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, c
     else len = len > DCAP ? DCAP : (len < DNEG ? DNEG : len);
     long long cand = (long long)dv + len;
     if (cand > DCAP) cand = DCAP;
+    if (!PR && cand >= k.bnd) return;   // bounded update: beyond every excess node
     if (PR && cand < DNEG) {
         cand = DNEG;
         atomicOr(&s_.flag, F_NEG);
@@ -556,7 +562,7 @@ __device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, c
 template <int W, bool PR>
 __device__ __forceinline__ void bf_node(const CellArgs& A, K& k, int nb, int v, Tc& t) {
     const int dv = dst(k)[v - k.x0];
-    if (!PR && dv >= DINF) return;
+    if (!PR && dv >= k.bnd) return;   // (k.bnd ≤ DINF: unreached nodes too)
     const int me = W == 64 ? lane() : (int)threadIdx.x;
     const long long pv = prc()[v - k.x0];
     int b0, en;
@@ -720,7 +726,7 @@ __device__ __forceinline__ void bf_leaf(const CellArgs& A, K& k, int nb, const i
         const Pos Q = dec(A, k, qr[u]);
         if (b0[u] + lig >= en[u]) continue;
         const int dv = dst(k)[v[u] - k.x0];
-        if (!PR && dv >= DINF) continue;
+        if (!PR && dv >= k.bnd) continue;
         relax_q<PR>(A, k, nb, Q, dv, prc()[v[u] - k.x0]);
         ++t.c[C_GUSCAN];
     }
@@ -833,7 +839,7 @@ __device__ __forceinline__ void bf_thr(const CellArgs& A, K& k, int nb, int v, T
     int b0;
     int4 qr[MAXP];
     int cnt = thr_load<MAXP>(A, k, v, b0, qr);
-    if (!PR && dv >= DINF) cnt = 0;
+    if (!PR && dv >= k.bnd) cnt = 0;
     t.c[C_GUSCAN] += cnt;
     unsigned m = 0;   // positions whose reverse (an in-arc of v) is residual
 #pragma unroll
@@ -1108,6 +1114,8 @@ __device__ __forceinline__ void control_body(const CellArgs& A, int N) {
     if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
     switch (c.op) {
         case O_SAT:
+            s_.bnd = DINF;
+            s_.nbx = 0;
             c.op = O_GUINIT;
             return;
         case O_GUINIT:
@@ -1126,6 +1134,8 @@ __device__ __forceinline__ void control_body(const CellArgs& A, int N) {
             return;
         case O_GUFIN: {
             ++c.updates;
+            s_.bnd = DINF;   // the next update lists its excess nodes afresh
+            s_.nbx = 0;
             if (s_.flag & F_INFEAS) return finish(CS_INFEASIBLE);
             const int n = c.nexc;
             if (n == 0) return phase_end(A);
@@ -1220,7 +1230,25 @@ __device__ __forceinline__ void gu_init(const CellArgs& A, const K& k) {
         const long long e = ld_ex(A, x);
         D[l] = e < 0 ? 0 : DINF;
         if (e < 0) mark(A, k, 0, x);
+        if (A.bound && e > 0) {
+            const int i = atomicAdd(&s_.nbx, 1);
+            if (i < BXC) s_.bx[i] = l;
+        }
     }
+}
+// Bounded update (the engine's k_gu_max bound): once every listed excess
+// node is reached, B = their largest tentative distance, and offers at or above B
+// are dropped. Every node below B is still exact (lengths are ≥ 0), excess nodes
+// included, and gu_fin caps L at B, so min(d, L) keeps the triangle inequality.
+// B only falls, so a stale copy read during a round is safe. After a step's barrier.
+__device__ __forceinline__ void gu_bound(const K& k) {
+    if (threadIdx.x >= 64) return;
+    const int n = s_.nbx;
+    if (n == 0 || n > BXC) return;
+    const int ln = (int)threadIdx.x;
+    const long long d = ln < n ? (long long)dst(k)[s_.bx[ln]] : 0;
+    const long long b = g_max<64>(d);
+    if (ln == 0 && b < (long long)s_.bnd) s_.bnd = (int)b;
 }
 // L = the largest finite distance; p ← p − ε·min(d, L); the excess nodes are
 // buffer 0 (an excess node the update did not reach: infeasible)
@@ -1231,6 +1259,7 @@ __device__ __forceinline__ void gu_fin(const CellArgs& A, const K& k) {
     for (int l = threadIdx.x; l < k.N; l += CT)
         if (D[l] < DINF) L = max(L, (long long)D[l]);
     L = blk_max(L);
+    if (L > (long long)k.bnd) L = k.bnd;
     const long long lim = (1LL << 60) / k.eps;
     if (L > lim) L = lim;
     int nexc = 0;
@@ -1268,6 +1297,8 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         s_.flag = 0;
         s_.stop = 0;
         s_.next = 0;
+        s_.bnd = DINF;
+        s_.nbx = 0;
         Ctl& c = c_;
         c = Ctl{};
         c.t0 = __builtin_amdgcn_s_memrealtime();
@@ -1328,6 +1359,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         k.eps = c_.eps;
         k.eps_shift = (k.eps & (k.eps - 1)) == 0 ? __builtin_ctzll((unsigned long long)k.eps) : -1;
         k.sp = c_.sp;
+        k.bnd = s_.bnd;
         const int src = c_.src, nb = c_.nb;
         switch (op) {
             case O_SAT:
@@ -1371,7 +1403,10 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
                 break;
         }
         __syncthreads();
-        if (op == O_BF) step_post<OP_BF>(A, k, src);
+        if (op == O_BF) {
+            step_post<OP_BF>(A, k, src);
+            gu_bound(k);
+        }
         else if (op == O_SWEEP) step_post<OP_SWEEP>(A, k, src);
         else if (op == O_PR) step_post<OP_PR>(A, k, src);
         if (threadIdx.x == 0) control(A, N);

@@ -4393,6 +4393,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.use_pr = use_pr ? 1 : 0;
         a.pr_cap = pr_cap;
         a.gi = gi_base;
+        a.bound = o.bf_bound < 0 ? 0 : 1;
         a.phase_exit = phase_exit;
         a.phase_frac = phase_frac;
         a.mode = mode;
