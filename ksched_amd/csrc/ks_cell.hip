@@ -51,7 +51,7 @@ constexpr long long DCAP = 1LL << 30;      // distances saturate here
 constexpr long long DNEG = -(1LL << 30);   // price refinement below this: treated as a negative cycle
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr size_t LDS_LIMIT = 163840;       // one workgroup may declare all 160 KiB on gfx950
-constexpr int BXC = 64;                    // updates with at most this many excess nodes are bounded
+constexpr int BXC = 256;                   // updates with at most this many excess nodes are bounded
 
 enum { OP_SWEEP = 0, OP_BF = 1, OP_PR = 2, OP_SAT = 3 };
 enum { F_INFEAS = 1, F_NEG = 2 };
@@ -1246,7 +1246,8 @@ __device__ __forceinline__ void gu_bound(const K& k) {
     const int n = s_.nbx;
     if (n == 0 || n > BXC) return;
     const int ln = (int)threadIdx.x;
-    const long long d = ln < n ? (long long)dst(k)[s_.bx[ln]] : 0;
+    long long d = 0;
+    for (int i = ln; i < n; i += 64) d = max(d, (long long)dst(k)[s_.bx[i]]);
     const long long b = g_max<64>(d);
     if (ln == 0 && b < (long long)s_.bnd) s_.bnd = (int)b;
 }
