@@ -149,7 +149,10 @@ typedef struct ks_opts {
                                   since the last solve (ksched's ageing of unscheduled
                                   arcs) is priced down by the rise, so that arc keeps its
                                   reduced cost [0: on]; < 0 off                          */
-    int32_t  reserved[2];
+    int32_t  warm_canon;       /* warm start: each solve ends by replacing its prices with
+                                  the flow's canonical ones (a Bellman-Ford at ε = 1 from
+                                  d = p), so carried prices do not drift [0: on]; < 0 off */
+    int32_t  reserved[1];
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */

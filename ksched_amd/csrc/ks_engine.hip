@@ -1689,8 +1689,8 @@ __global__ void k_gu_init(DG g, int seq0, int list) {
         }
 }
 
-// PR init: dist = 0 everywhere.
-__global__ void k_pr_init(DG g, int seq0) {
+// PR init: dist = 0 everywhere, or dist = p (canonical prices: see k_pr_apply).
+__global__ void k_pr_init(DG g, int seq0, int from_p) {
     clear_fronts(g, g.bf);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         g.ctl->bf_done = 0;
@@ -1698,7 +1698,7 @@ __global__ void k_pr_init(DG g, int seq0) {
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
-        g.dist[ni(v)] = 0;
+        g.dist[ni(v)] = from_p ? g.p0[ni(v)] : 0;
 }
 
 // End of a cycle: an update that has not converged is continued by the next
@@ -2371,7 +2371,11 @@ __global__ void k_perturb_price(DG g, int x, long long delta) {
     }
 }
 
-// PR success: p ← p − ε·d (d ≤ 0).
+// PR success: p ← p − ε·d. From d ≡ 0 (d ≤ 0) prices only rise, keeping their
+// history. From d = p at ε = 1 the fixpoint is d(u) = p(u) + min(0, min_w dist(u, w))
+// over residual paths of length cost + 1 per arc, so p − d = −min(0, min_w dist(u, w)):
+// the canonical prices of the flow, the same for any prices it started from
+// (warm_canon: the drift of carried prices).
 __global__ void k_pr_apply(DG g) {
     if (!g.ctl->bf_done) return;
     const long long eps = g.ctl->eps;
@@ -4098,10 +4102,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         }
     };
     // Price refinement at eps_try: 1 = success (prices updated), 0 = failed, <0 error.
-    auto price_refine = [&](long long eps_try, int* rounds_used, int cap) -> int {
+    auto price_refine = [&](long long eps_try, int* rounds_used, int cap, int from_p = 0) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(set_eps(eps_try));
-        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
+        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, from_p);
         int used = 0, ok = 0;
         for (int batch = 0; used < cap; ++batch) {
             const int k = std::min(64, cap - used);
@@ -4597,6 +4601,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             status = KS_E_VERIFY;
             err = std::string("on-device verification failed (") + ((bad & 1) ? "capacity " : "") +
                   ((bad & 2) ? "optimality " : "") + ((bad & 4) ? "conservation" : "") + ")";
+        }
+        // warm starts: replace the carried prices by the flow's canonical ones (the
+        // next round starts from prices without history). Kept only if the
+        // Bellman-Ford converges; the certificate holds either way.
+        if (status == KS_OK && !bad && o.warm_start > 0 && o.warm_canon >= 0 && !s.cell_layout) {
+            int used = 0;
+            const int pr = price_refine(1, &used, 4 * pr_cap, 1);
+            if (pr < 0) return pr;
+            if (cycle_log) std::fprintf(stderr, "canonical prices: %s after %d rounds\n", pr ? "set" : "not converged", used);
         }
     }
     KS_CHECK(hipEventRecord(s.ev[7], st));

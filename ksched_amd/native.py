@@ -53,7 +53,8 @@ class KsOpts(C.Structure):
                 ("fault_inject", C.c_int32), ("walk_passes", C.c_int32), ("tail_nodes", C.c_int32),
                 ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32), ("cell_nodes", C.c_int32),
                 ("warm_shift", C.c_int32),
-                ("reserved", C.c_int32 * 2)]
+                ("warm_canon", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 class KsResult(C.Structure):
