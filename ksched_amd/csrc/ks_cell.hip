@@ -1087,30 +1087,32 @@ __device__ __forceinline__ void phase_end(const CellArgs& A) {
     }
 }
 
-__device__ __forceinline__ void control_body(const CellArgs& A, int N);
+__device__ __forceinline__ void control_body(const CellArgs& A, int N, unsigned long long now);
+// One clock read per operation (a scalar-memory round trip on thread 0, between
+// the workgroup's two barriers): the operation's time, the timeout, the next start.
 __device__ __forceinline__ void control(const CellArgs& A, int N) {
     Ctl& c = c_;
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     if (c.op == O_SWEEP || c.op == O_BF) {
         const int f = c.fsz;
         const int b = f <= 16 ? 0 : f <= 64 ? 1 : f <= 256 ? 2 : f <= 1024 ? 3 : f <= 4096 ? 4 : 5;
         const int h = (c.op == O_BF ? 6 : 0) + b;
-        c.hist_t[h] += __builtin_amdgcn_s_memrealtime() - c.t_op;
+        c.hist_t[h] += now - c.t_op;
         ++c.hist_n[h];
     }
-    control_body(A, N);
+    control_body(A, N, now);
     c.fsz = c.src < 2 ? total_any(c.src) : N;
 }
-__device__ __forceinline__ void control_body(const CellArgs& A, int N) {
+__device__ __forceinline__ void control_body(const CellArgs& A, int N, unsigned long long now) {
     Ctl& c = c_;
     s_.next = 0;   // the next step's item dispenser (read after the barrier that follows)
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     c.op_ticks[c.op] += now - c.t_op;
     if (t_items_ > c.t_op) c.item_ticks[c.op] += t_items_ - c.t_op;
     if (t_first_ > c.t_op && t_first_ != ~0ULL) c.first_ticks[c.op] += t_first_ - c.t_op;
     ++c.op_n[c.op];
     t_items_ = 0;
     t_first_ = ~0ULL;
-    c.t_op = __builtin_amdgcn_s_memrealtime();
+    c.t_op = now;
     if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
     switch (c.op) {
         case O_SAT:
