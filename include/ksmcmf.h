@@ -134,7 +134,8 @@ typedef struct ks_opts {
     int32_t  fwd_nodes;        /* in a coarse phase (one a finer phase follows), once
                                   ≤ fwd_nodes nodes hold excess, a cycle searches from them
                                   to the nearest deficit and pushes along the search's
-                                  shortest paths instead of a global update [64]; a search
+                                  shortest paths instead of a global update [32 below
+                                  32,768 nodes, else 64]; a search
                                   whose frontier grows past n/4 nodes, or that runs longer
                                   than twice the last global update's rounds, costs ONE
                                   global update and the next cycle searches forward again.

@@ -4023,7 +4023,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // forward tail updates once ≤ fwd_k nodes hold excess (ks_opts.fwd_nodes; the
     // search key packs an arc position into FS_PB bits)
     const bool use_fwd = o.fwd_nodes >= 0 && s.m2cap < FS_NONE;
-    const int fwd_k = o.fwd_nodes > 0 ? (int)o.fwd_nodes : 64;
+    // (default by size: config 2's 12k-node searches widen sooner; interleaved A/B,
+    // config 2 28.0 / 26.4 → 25.5 / 25.0 ms at 32, config 4 slower at 32 than at 64)
+    const int fwd_k = o.fwd_nodes > 0 ? (int)o.fwd_nodes : (nn < 32768 ? 32 : 64);
     int kf = 16;                        // forward rounds enqueued per cycle (adaptive)
     uint64_t fwd_updates = 0, fs_launches = 0;
     const int alpha = o.alpha >= 2 ? o.alpha : 8;
