@@ -542,13 +542,26 @@ __device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, c
     const long long pu = prc()[lu];
     int* D = dst(k);
     const long long x = pu - q.cost - pv;
-    long long len = PR ? x + 1 : (k.eps_shift >= 0 ? (x >> k.eps_shift) : floordiv(x, k.eps)) + 1;
-    if (!PR) len = len < 0 ? 0 : (len > DCAP ? DCAP : len);
-    else len = len > DCAP ? DCAP : (len < DNEG ? DNEG : len);
+    if (!PR) {
+        // global update, in 32 bits past the price difference: len = clamp(⌊x/ε⌋ + 1,
+        // 0, DCAP) and a reached dv ≤ DCAP, so dv + len ≤ 2^31 fits an unsigned word
+        const long long lq = k.eps_shift >= 0 ? (x >> k.eps_shift) : floordiv(x, k.eps);
+        const unsigned len = lq < 0 ? 0u : (lq >= DCAP - 1 ? (unsigned)DCAP : (unsigned)lq + 1u);
+        unsigned c = (unsigned)dv + len;
+        c = c > (unsigned)DCAP ? (unsigned)DCAP : c;
+        const int cand = (int)c;
+        if (cand >= k.bnd) return;   // bounded update: beyond every excess node
+        if (cand < D[lu]) {
+            const int old = atomicMin(&D[lu], cand);
+            if (cand < old) mark(A, k, nb, q.head);
+        }
+        return;
+    }
+    long long len = x + 1;
+    len = len > DCAP ? DCAP : (len < DNEG ? DNEG : len);
     long long cand = (long long)dv + len;
     if (cand > DCAP) cand = DCAP;
-    if (!PR && cand >= k.bnd) return;   // bounded update: beyond every excess node
-    if (PR && cand < DNEG) {
+    if (cand < DNEG) {
         cand = DNEG;
         atomicOr(&s_.flag, F_NEG);
     }
