@@ -13,18 +13,21 @@ from oracle import ko
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("warm,shift,path", [(0, 0, "engine"), (1, 0, "engine"), (2, 0, "engine"),
-                                              (2, -1, "engine"), (0, 0, "cell"), (2, 0, "cell")])
-def test_incremental_rounds_match_full_resolve(warm, shift, path):
+@pytest.mark.parametrize("warm,shift,path,canon", [(0, 0, "engine", 0), (1, 0, "engine", 0), (2, 0, "engine", 0),
+                                                    (2, -1, "engine", 0), (2, 0, "engine", -1), (0, 0, "cell", 0),
+                                                    (2, 0, "cell", 0)])
+def test_incremental_rounds_match_full_resolve(warm, shift, path, canon):
     """Config 4 at config-2 scale: pins, completions, arrivals, ageing and
     capacity refresh as one delta stream per round; the device result after
     applying the deltas equals the oracle on the cell's full graph, re-solved
     from scratch (warm_start 0) or from the previous flow and prices (1: the
     first phase saturates only violations, 2: every phase does; warm_shift −1
-    turns off the price shift that absorbs the ageing), on the multi-kernel
-    engine and on the cell solver."""
+    turns off the price shift that absorbs the ageing; warm_canon −1 keeps the
+    prices each solve ends with instead of the flow's canonical ones), on the
+    multi-kernel engine and on the cell solver."""
     cell = churn.Cell(10_000, 1_000, 25, 100, 2)
-    ctx = native.Context(0, warm_start=warm, warm_shift=shift, cell_nodes=-1 if path == "engine" else CELL_ANY)
+    ctx = native.Context(0, warm_start=warm, warm_shift=shift, warm_canon=canon,
+                         cell_nodes=-1 if path == "engine" else CELL_ANY)
     ctx.load_graph(cell.graph())
     r = ctx.solve()
     mp = ctx.task_mapping()
