@@ -104,7 +104,8 @@ typedef struct ks_opts {
                                   ≤ walk_slack·ε toward a smaller distance while ε > 1
                                   [4]; < 0 disables the walkers                       */
     int32_t  final_div;        /* the phase price refinement certifies runs at 1/final_div
-                                  of a cost unit [48]; < 0: the plain max|cost|/α^k ladder */
+                                  of a cost unit [20 for cells and graphs under 32,768
+                                  nodes, else 48]; < 0: the plain max|cost|/α^k ladder   */
     int32_t  pr_rounds;        /* Bellman-Ford rounds one price refinement may take [160] */
     int32_t  phase_exit;       /* a coarse phase ends once ≤ phase_exit nodes hold excess
                                   [256] ... */

@@ -4056,14 +4056,18 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int phase_exit = o.phase_exit < 0 ? 0 : (o.phase_exit > 0 ? o.phase_exit : 256);
     const int phase_frac = o.phase_frac > 0 ? o.phase_frac : 128;
     // ε schedule: the phase that price refinement certifies runs at 1/D of a cost
-    // unit (D = 48; ks_opts.final_div), the others at α-multiples of it, the first in
-    // [max|cost|/α², max|cost|/α) scaled. Measured on config 3 (40 solves each):
-    // ending at 1/32 of a unit (the plain max|cost|/α^k sequence) left the flow
-    // short of optimal in 15 of 40 solves — a sixth phase, ≈ 28 ms — at 1/48 in
-    // none; 1/64 and 1/96 cost more per phase.
+    // unit (ks_opts.final_div), the others at α-multiples of it, the first in
+    // [max|cost|/α², max|cost|/α) scaled. D = 48 on large graphs. Measured on config 3
+    // (40 solves each): ending at 1/32 of a unit (the plain max|cost|/α^k sequence)
+    // left the flow short of optimal in 15 of 40 solves — a sixth phase, ≈ 28 ms —
+    // at 1/48 in none; 1/64 and 1/96 cost more per phase. D = 20 on small graphs and
+    // cells (under 32,768 nodes; every cell is): their flow is usually optimal a
+    // phase earlier (config 2 26–27 → 20–21 ms, config 5 53–54 → 41–43 ms).
     long long eps = std::max<long long>(1, maxc * mult);
     {
-        const long long D = o.final_div < 0 ? 0 : (o.final_div > 0 ? o.final_div : 48);
+        const long long D = o.final_div < 0 ? 0
+                            : o.final_div > 0 ? o.final_div
+                            : (s.cell_layout || nn < 32768) ? 20 : 48;
         if (D > 0 && use_pr && maxc > 0) {
             long long e = std::max<long long>(1, (mult - 1) / D);
             // the cell solver's ladder is powers of two (α = 8): its arc lengths
