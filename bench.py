@@ -542,7 +542,8 @@ def run_batch(args, D):
     if args.batch_mode == "abi":
         tg0 = time.perf_counter()
         pu, cost, flow = bt.gather(T, root=D.rank == 0)
-        gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "via": "RCCL ncclSend/ncclRecv in libksmcmf",
+        gather = {"ms": round(1e3 * (time.perf_counter() - tg0), 3), "via": ("RCCL ncclSend/ncclRecv in libksmcmf" if D.world > 1
+                                                                   else "none (world 1: rank 0's own rows, no RCCL call)"),
                   "bytes_per_rank": batch.slots_per_rank(num, D.world) * (T + 2) * 8}
         if D.rank == 0:
             per_graph = cost

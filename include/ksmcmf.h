@@ -123,7 +123,9 @@ typedef struct ks_opts {
                                   Both must be repaired by the certificate recovery.
                                   Bit 2 (ks_batch_create*): global rank 0 fails to pack
                                   its rows in ks_batch_gather (every rank must still
-                                  reach the collective and return the error).          */
+                                  reach the collective and return the error). Bit 3
+                                  (ks_batch_create*): rank 0's receive buffer
+                                  allocation fails in ks_batch_gather (the same).     */
     int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
                                   cycle [1]; later passes retry units left short        */
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —
@@ -153,7 +155,9 @@ typedef struct ks_opts {
                                   reduced cost [0: on]; < 0 off                          */
     int32_t  warm_canon;       /* warm start: each solve ends by replacing its prices with
                                   the flow's canonical ones (a Bellman-Ford at ε = 1 from
-                                  d = p), so carried prices do not drift [0: on]; < 0 off */
+                                  d = p), so carried prices do not drift [0: on]; < 0 off.
+                                  Multi-kernel engine only: a cell-solver solve keeps the
+                                  prices its workgroup ended with                      */
     int32_t  reserved[1];
 } ks_opts;
 
@@ -234,7 +238,11 @@ typedef struct ks_result {
     uint64_t cell_ticks_max;   /* slowest cell's in-kernel solve time (100 MHz ticks)   */
     uint64_t cell_ticks_sum;   /* Σ over cells of their in-kernel solve times            */
     uint64_t fs_arc_scans;     /* residual out-arcs the forward tail searches examined    */
-    uint64_t reserved2[3];
+    uint64_t cell_fallbacks;   /* cells of this solve that did not converge in the cell
+                                  solver (step cap or wall-clock limit) and were re-solved
+                                  on the multi-kernel engine, the other cells' optima
+                                  kept (the status stays KS_OK)                         */
+    uint64_t reserved2[2];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

@@ -124,6 +124,7 @@ struct ks_batch {
     long long* root_buf = nullptr;      // rank 0: world × slots × rowlen
     size_t root_cap = 0;
     int fault_pack = 0;                 // TESTS ONLY (ks_opts.fault_inject bit 2): global rank + 1 whose packing fails
+    int fault_root = 0;                 // TESTS ONLY (ks_opts.fault_inject bit 3): rank 0's receive buffer allocation fails
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -138,17 +139,13 @@ namespace {
         hipError_t _e = (expr);                                               \
         if (_e != hipSuccess) return b->fail(KS_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
-#define KB_NCCL(expr)                                                         \
-    do {                                                                      \
-        ncclResult_t _r = (expr);                                             \
-        if (_r != ncclSuccess) return b->fail(KS_E_DEVICE, std::string(#expr) + ": " + rccl().GetErrorString(_r)); \
-    } while (0)
 
 ks_batch* make_batch(int world, const ks_opts* opts, const std::vector<std::pair<int, int>>& dev_rank) {
     ks_batch* b = new (std::nothrow) ks_batch;
     if (!b) return nullptr;
     b->world = world;
     b->fault_pack = (opts && (opts->fault_inject & 4)) ? 1 : 0;   // TESTS ONLY: global rank 0's packing fails
+    b->fault_root = (opts && (opts->fault_inject & 8)) ? 1 : 0;   // TESTS ONLY: rank 0's root buffer allocation fails
     for (auto [dev, rank] : dev_rank) {
         ks_batch::Local l;
         l.device = dev;
@@ -333,6 +330,7 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
     const size_t rowlen = kb_rowlen(max_tasks);
     const size_t block = kb_block(b->ngraphs, b->world, max_tasks);   // elements per rank
     bool has_root = false;
+    int root_loc = -1;   // the local device of global rank 0 once its receive buffer is ready
     // 1. every device packs its block: [status][rows: cost, flow value, cell-local PU per task].
     //    A rank that fails here — a logical error or ANY HIP failure — still takes part
     //    in the collective below with its status word set, so its peers never wait for
@@ -407,14 +405,42 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
                                    dim3(256), 0, st, (int)k, (int)rowlen, (const long long*)doff, l.rows);
             KB_TRY(hipGetLastError());
         }
-        KB_TRY(hipStreamSynchronize(st));
+        // rank 0 also holds the receive buffer of step 3: allocated (and its own block
+        // copied in) here, so a failure is this rank's status word like any other and
+        // nothing between the status all-reduce and the send/receive group can fail
+        if (rc == KS_OK && l.grank == 0) {
+            const size_t need = block * (size_t)b->world;
+            if (b->fault_root) {   // TESTS ONLY: the root buffer's allocation fails
+                rc = KS_E_DEVICE;
+                c->err = "injected root buffer allocation failure";
+            } else if (b->root_cap < need) {
+                if (b->root_buf) (void)hipFree(b->root_buf);
+                b->root_buf = nullptr;
+                b->root_cap = 0;
+                KB_TRY(hipMalloc(&b->root_buf, need * sizeof(long long)));
+                if (rc == KS_OK) b->root_cap = need;
+            }
+            if (rc == KS_OK) root_loc = (int)li;
+            KB_TRY(hipMemcpyAsync(b->root_buf, l.rows, block * sizeof(long long), hipMemcpyDeviceToDevice, st));
+        }
+        // always drain the stream, also after a failure: the memset, the copies and
+        // k_localize must be finished before the status word is written or we return
+        {
+            const hipError_t se = hipStreamSynchronize(st);
+            if (se != hipSuccess && rc == KS_OK) {
+                rc = KS_E_DEVICE;
+                c->err = std::string("hipStreamSynchronize: ") + hipGetErrorString(se);
+            }
+        }
         if (rc != KS_OK) {
             status[li] = rc;
             if (first_err.empty()) first_err = "rank " + std::to_string(l.grank) + ": " + c->err;
             // the status word goes out in the block when the rows buffer exists
+            // (written on the engine's stream, which the rows' producers used)
             if (l.rows) {
                 const long long sw = rc;
-                (void)hipMemcpy(l.rows, &sw, sizeof(long long), hipMemcpyHostToDevice);
+                if (hipMemcpyAsync(l.rows, &sw, sizeof(long long), hipMemcpyHostToDevice, st) == hipSuccess)
+                    (void)hipStreamSynchronize(st);
             }
         }
 #undef KB_TRY
@@ -433,10 +459,16 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
                 if (first_err.empty()) first_err = "rank " + std::to_string(l.grank) + ": status word not posted";
             }
         }
-        KB_NCCL(rccl().GroupStart());
-        for (auto& l : b->loc)
-            KB_NCCL(rccl().AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream()));
-        KB_NCCL(rccl().GroupEnd());
+        {   // (the group is always closed: an RCCL error is returned after GroupEnd)
+            ncclResult_t nr = rccl().GroupStart();
+            for (auto& l : b->loc) {
+                const ncclResult_t x = rccl().AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream());
+                if (nr == ncclSuccess) nr = x;
+            }
+            const ncclResult_t ge = rccl().GroupEnd();
+            if (nr == ncclSuccess) nr = ge;
+            if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("status all-reduce: ") + rccl().GetErrorString(nr));
+        }
         long long worst = 0;
         for (size_t li = 0; li < b->loc.size(); ++li) {
             auto& l = b->loc[li];
@@ -454,33 +486,27 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
     // world 1: this process's own failure ends it here (no peer waits)
     for (int rc : status)
         if (rc != KS_OK) return b->fail(rc, first_err);
-    // 3. one group: every rank's block to global rank 0
-    long long* rbuf = nullptr;
-    for (auto& l : b->loc)
-        if (l.grank == 0) {
-            KB_HIP(hipSetDevice(l.device));
-            const size_t need = block * (size_t)b->world;
-            if (b->root_cap < need) {
-                if (b->root_buf) (void)hipFree(b->root_buf);
-                b->root_buf = nullptr;
-                KB_HIP(hipMalloc(&b->root_buf, need * sizeof(long long)));
-                b->root_cap = need;
-            }
-            rbuf = b->root_buf;
-            KB_HIP(hipMemcpyAsync(rbuf, l.rows, block * sizeof(long long), hipMemcpyDeviceToDevice, l.ctx->eng.stream()));
-        }
+    // 3. one group: every rank's block to global rank 0. Nothing between the status
+    //    all-reduce and GroupEnd returns early: an RCCL error is remembered and
+    //    returned after the group, so no peer is left waiting in a send.
+    long long* rbuf = root_loc >= 0 ? b->root_buf : nullptr;
     if (b->world > 1) {
-        KB_NCCL(rccl().GroupStart());
+        ncclResult_t nr = rccl().GroupStart();
         for (auto& l : b->loc) {
             hipStream_t st = l.ctx->eng.stream();
             if (l.grank == 0) {
-                for (int r = 1; r < b->world; ++r)
-                    KB_NCCL(rccl().Recv(rbuf + (size_t)r * block, block, ncclInt64, r, l.comm, st));
+                for (int r = 1; r < b->world; ++r) {
+                    const ncclResult_t x = rccl().Recv(rbuf + (size_t)r * block, block, ncclInt64, r, l.comm, st);
+                    if (nr == ncclSuccess) nr = x;
+                }
             } else {
-                KB_NCCL(rccl().Send(l.rows, block, ncclInt64, 0, l.comm, st));
+                const ncclResult_t x = rccl().Send(l.rows, block, ncclInt64, 0, l.comm, st);
+                if (nr == ncclSuccess) nr = x;
             }
         }
-        KB_NCCL(rccl().GroupEnd());
+        const ncclResult_t ge = rccl().GroupEnd();
+        if (nr == ncclSuccess) nr = ge;
+        if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("ncclSend/ncclRecv group: ") + rccl().GetErrorString(nr));
     }
     for (auto& l : b->loc) {
         KB_HIP(hipSetDevice(l.device));

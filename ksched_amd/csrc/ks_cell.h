@@ -115,14 +115,17 @@ struct CellArgs {
     int diag;                // per-item / per-class timing for the cycle log (ks_opts.log_cycles)
     int bound;               // 1: bounded global updates (ks_opts.bf_bound >= 0)
     const int* bad;          // set by k_cell_pack: a value the compact record cannot hold
+    int fault_cell;          // TESTS ONLY (ks_opts.fault_inject bit 4): this cell stops after
+    int fault_ops;           //   fault_ops operations with CS_NOCONV (−1: none)
 };
 
-// LDS one workgroup needs for cells of up to n nodes (0 when they do not fit).
-size_t cell_lds_bytes(int n);
+// LDS one workgroup needs for cells of up to n nodes (0 when they do not fit in
+// limit bytes: the device's opt-in LDS per workgroup, 160 KiB on gfx950).
+size_t cell_lds_bytes(int n, size_t limit);
 // Largest cell the LDS holds (and the compact record's head field addresses).
-int cell_max_nodes();
+int cell_max_nodes(size_t limit);
 // k_cell_pack → k_cell → k_cell_unpack on st; *bad (device int) is set when a
 // position does not fit the compact record (every cell then returns CS_RANGE).
-hipError_t cell_launch(const CellArgs& a, int* bad, hipStream_t st);
+hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st);
 
 }  // namespace ks

@@ -50,7 +50,6 @@ constexpr int DINF = 0x7fffffff;           // not reached by the update
 constexpr long long DCAP = 1LL << 30;      // distances saturate here
 constexpr long long DNEG = -(1LL << 30);   // price refinement below this: treated as a negative cycle
 constexpr long long INF64 = 0x3fffffffffffffffLL;
-constexpr size_t LDS_LIMIT = 163840;       // one workgroup may declare all 160 KiB on gfx950
 constexpr int BXC = 256;                   // updates with at most this many excess nodes are bounded
 
 enum { OP_SWEEP = 0, OP_BF = 1, OP_PR = 2, OP_SAT = 3 };
@@ -1127,6 +1126,13 @@ __device__ __forceinline__ void control_body(const CellArgs& A, int N, unsigned 
     t_first_ = ~0ULL;
     c.t_op = now;
     if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
+    // TESTS ONLY: one cell gives up part-way, as a step cap would (the host then
+    // re-solves that cell alone on the engine)
+    if ((int)blockIdx.x == A.fault_cell) {
+        unsigned ops = 0;
+        for (int i = 0; i < O_DONE; ++i) ops += c.op_n[i];
+        if ((int)ops >= A.fault_ops) return finish(CS_NOCONV);
+    }
     switch (c.op) {
         case O_SAT:
             s_.bnd = DINF;
@@ -1512,27 +1518,27 @@ __global__ void k_cell_unpack(CellArgs A, const int* bad) {
 
 }  // namespace
 
-size_t cell_lds_bytes(int n) {
+size_t cell_lds_bytes(int n, size_t limit) {
     if (n < 0) return 0;
     const size_t w = ((size_t)n + 31) / 32;
     // prices 8n, distances 4n rounded up to whole 8-byte words, two bitmaps
     const size_t b = 8 * (size_t)n + 8 * (((size_t)n + 1) / 2) + 2 * 4 * w;
     const size_t dyn = (b + 15) / 16 * 16;
-    return dyn + sizeof(St) + sizeof(Ctl) + 64 + sizeof(cls_t_) + sizeof(cls_n_) <= LDS_LIMIT ? dyn : 0;
+    return dyn + sizeof(St) + sizeof(Ctl) + 64 + sizeof(cls_t_) + sizeof(cls_n_) <= limit ? dyn : 0;
 }
 
-int cell_max_nodes() {
-    int lo = 0, hi = 1 << 16;
+int cell_max_nodes(size_t limit) {
+    int lo = 0, hi = 1 << CELL_HEAD_BITS;   // (the compact record's local head field)
     while (hi - lo > 1) {
         const int mid = (lo + hi) / 2;
-        if (cell_lds_bytes(mid)) lo = mid;
+        if (cell_lds_bytes(mid, limit)) lo = mid;
         else hi = mid;
     }
     return lo;
 }
 
-hipError_t cell_launch(const CellArgs& a, int* bad, hipStream_t st) {
-    const size_t lds = cell_lds_bytes(a.max_nodes);
+hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st) {
+    const size_t lds = cell_lds_bytes(a.max_nodes, lds_limit);
     if (!lds || a.ncells <= 0) return hipErrorInvalidValue;
     // (per device and cheap: set on every launch)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cell),

@@ -2488,6 +2488,24 @@ __global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive,
     }
 }
 
+// Per-cell fallback: the cells in rng (node-slot ranges [lo, hi),
+// nr of them) restart cold on the multi-kernel engine — their arcs' carried flows
+// and their nodes' carried prices are zeroed between the save and the restore.
+__global__ void k_fb_reset(int hi, int ncap, int nr, const long long* __restrict__ rng, const int* __restrict__ a_src,
+                           long long* __restrict__ saved, long long* __restrict__ pslot) {
+    const long long n = hi > ncap ? hi : ncap;
+    for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < n; i += (long long)gridDim.x * BLK) {
+        const long long vs = i < hi ? a_src[i] : -1, vn = i < ncap ? i : -1;
+        bool rs = false, rn = false;
+        for (int r = 0; r < nr; ++r) {
+            rs |= vs >= rng[2 * r] && vs < rng[2 * r + 1];
+            rn |= vn >= rng[2 * r] && vn < rng[2 * r + 1];
+        }
+        if (rs) saved[i] = 0;
+        if (rn) pslot[i] = 0;
+    }
+}
+
 __global__ void k_save_prices(int ncap, const int* __restrict__ perm, const long long* __restrict__ p0,
                               long long* __restrict__ pslot) {
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK)
@@ -2836,6 +2854,10 @@ struct EngineImpl {
     DBuf<CellPos> cl_pos;               // compact positions (k_cell_pack / k_cell_unpack)
     DBuf<int> cl_bad;
     bool cell_refused = false;          // the graph's values do not fit the compact record: engine until reload
+    size_t lds_limit = 0;               // the device's opt-in LDS per workgroup (sizes the cells)
+    bool fb_active = false;             // a per-cell fallback solve is running (engine order, failing cells cold)
+    std::vector<int> fb_cells;          // the cells it re-solves
+    DBuf<long long> fb_rng;             // their node-slot ranges on the device
     std::vector<CellOut> h_cell_out;
     // ---- scheduler-side sweeps (ks_sched.hip)
     DBuf<int> sched_i;                  // int scratch
@@ -2890,7 +2912,7 @@ struct EngineImpl {
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
         map_scratch.release(); flow_recs.release();
         cells.release(); cl_lists.release(); cl_rln.release(); cl_rlp.release(); cl_out.release(); cl_pos.release();
-        cl_bad.release();
+        cl_bad.release(); fb_rng.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         for (auto* h : h_cyc)
             if (h) (void)hipHostFree(h);
@@ -3039,6 +3061,12 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     }
     KS_CHECK(hipSetDevice(device));
     KS_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    {   // LDS one workgroup may declare (the cell solver's size limit; 160 KiB on gfx950)
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess || v <= 0)
+            KS_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+        s.lds_limit = (size_t)std::max(v, 0);
+    }
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
     for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
     for (auto& c : s.cev)
@@ -3544,8 +3572,8 @@ void Engine::set_cells(const int64_t* off, size_t k) {
 // by side on separate CUs, so they take it up to the LDS limit.
 constexpr int64_t kCellSingleNodes = 4096;
 static bool want_cells(const EngineImpl& s) {
-    if (s.opts.cell_nodes < 0 || s.cell_refused) return false;
-    int64_t lim = std::min<int64_t>(cell_max_nodes(), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
+    if (s.opts.cell_nodes < 0 || s.cell_refused || s.fb_active) return false;
+    int64_t lim = std::min<int64_t>(cell_max_nodes(s.lds_limit), s.opts.cell_nodes > 0 ? s.opts.cell_nodes : INT32_MAX);
     if (s.opts.cell_nodes == 0 && s.cell_off.size() < 2) lim = std::min(lim, kCellSingleNodes);
     const int64_t ncap =
         s.csr_valid ? s.ncap : s.nslots + (s.incremental ? std::max<int64_t>(64, s.nslots / 16) : 0);
@@ -3923,7 +3951,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_host0).count();
     };
     hipStream_t st = s.stream;
-    const bool use_warm = warm && s.has_prev;
+    // a per-cell fallback carries the cell solver's state (the cells that converged
+    // keep their optima; the failing ones restart cold, k_fb_reset)
+    const bool fb = s.fb_active;
+    const bool use_warm = (warm && s.has_prev) || fb;
     s.solved = false;
     {   // the cell solver's node order, or the multi-kernel engine's (a change rebuilds the CSR)
         const bool cells_now = want_cells(s);
@@ -3935,6 +3966,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.warm_started = use_warm ? 1 : 0;
     res.rebuilt = s.csr_valid ? 0 : 1;
     res.recoveries = 0;
+    res.cell_fallbacks = 0;
     KS_CHECK(hipEventRecord(s.ev[0], st));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
@@ -3958,6 +3990,22 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                    s.saved_flows.p);
             hipLaunchKernelGGL(k_save_prices, dim3(grid_for(ncap_prev)), dim3(BLK), 0, st, (int)ncap_prev,
                                (const int*)s.perm.p, (const long long*)s.nd.p, s.p_slot.p);
+            if (fb && !s.fb_cells.empty()) {
+                std::vector<long long> rng;
+                const size_t kc = s.cell_off.size() >= 2 ? s.cell_off.size() - 1 : 1;
+                for (int c : s.fb_cells) {
+                    rng.push_back(kc > 1 ? s.cell_off[c] : 0);
+                    rng.push_back(kc > 1 ? s.cell_off[c + 1] : ncap_prev);
+                }
+                KS_CHECK(s.fb_rng.ensure(rng.size()));
+                KS_CHECK(hipMemcpyAsync(s.fb_rng.p, rng.data(), rng.size() * sizeof(long long), hipMemcpyHostToDevice,
+                                        st));
+                const int n = (int)std::max<int64_t>(hi0, ncap_prev);
+                hipLaunchKernelGGL(k_fb_reset, dim3(grid_for(std::max(n, 1))), dim3(BLK), 0, st, hi0, (int)ncap_prev,
+                                   (int)(rng.size() / 2), (const long long*)s.fb_rng.p, (const int*)s.a_src.p,
+                                   s.saved_flows.p, s.p_slot.p);
+                KS_CHECK(hipStreamSynchronize(st));   // (rng is a host vector)
+            }
         }
         int rc = build(s, err);
         if (rc) return rc;
@@ -4343,7 +4391,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // their out-arcs, then a start at a small ε (≤ 8 cost units) saturating only
     // the arcs that violate it
     long long warm_thr = 0;
-    if (use_warm) {
+    if (use_warm && !fb) {
         if (o.warm_shift >= 0)
             hipLaunchKernelGGL(k_price_shift, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, (int)s.ncap,
                                (const unsigned long long*)s.n_cshift.p, (const int*)s.perm.p, mult, s.nd.p);
@@ -4410,8 +4458,17 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.max_nodes = s.cell_max;
         a.timeout_ticks = (unsigned long long)(kCellLimitS * 1e8);
         a.diag = cycle_log ? 1 : 0;
+        // TESTS ONLY (fault_inject bit 4): the middle cell gives up after 40 operations
+        a.fault_cell = (o.fault_inject & 16) && mode == 0 ? ncells / 2 : -1;
+        a.fault_ops = 40;
         KS_CHECK(hipEventRecord(s.kev[2], st));
-        KS_CHECK(cell_launch(a, s.cl_bad.p, st));
+        {   // a launch the device refuses (e.g. its LDS) → the multi-kernel engine instead
+            const hipError_t le = cell_launch(a, s.cl_bad.p, s.lds_limit, st);
+            if (le != hipSuccess) {
+                (void)hipGetLastError();
+                return (int)CS_RANGE;
+            }
+        }
         KS_CHECK(hipEventRecord(s.kev[3], st));
         KS_CHECK(hipMemcpyAsync(s.h_cell_out.data(), s.cl_out.p, ncells * sizeof(CellOut), hipMemcpyDeviceToHost, st));
         KS_CHECK(hipStreamSynchronize(st));
@@ -4485,11 +4542,34 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             s.cell_refused = true;
             s.cell_layout = false;
             s.csr_valid = false;
+            // the warm start's price shift is already in the carried prices: the retry
+            // must not apply it a second time
+            if (use_warm) KS_CHECK(hipMemsetAsync(s.n_cshift.p, 0, s.nstore * sizeof(unsigned long long), st));
             return solve(res, warm, err);
         }
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
         ms_cycles += ev_ms(s.ev[3], s.ev[5]);
+        if (cs == CS_TIMEOUT || cs == CS_NOCONV) {
+            // Per-cell fallback: only the cells that gave up are solved again, on the
+            // multi-kernel engine (engine order, the state carried across the rebuild:
+            // the converged cells keep their optimal flows and prices, the failing ones
+            // restart cold). One hard cell no longer discards the batch.
+            std::vector<int> bad;
+            for (size_t i = 0; i < s.h_cell_out.size(); ++i)
+                if (s.h_cell_out[i].status == CS_TIMEOUT || s.h_cell_out[i].status == CS_NOCONV) bad.push_back((int)i);
+            s.fb_cells = bad;
+            s.fb_active = true;
+            s.cell_layout = false;
+            s.csr_valid = false;
+            const int rc = solve(res, warm, err);
+            s.fb_active = false;
+            s.fb_cells.clear();
+            res.cell_fallbacks = bad.size();
+            res.solver = 1;
+            res.cells = ncells;
+            return rc;
+        }
         if (int rc = cell_status(cs, "solve")) return rc;
         eps = 1;
     } else do {
@@ -4501,8 +4581,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // disturbs far less than saturating every negative arc.
         // warm_start 2: every phase of a warm solve saturates only the arcs that
         // violate its ε (the previous optimum's arcs in [−1, 0) stay as they are)
-        const long long sat_thr =
-            phases == 1 && use_warm ? warm_thr : ((pr_failed || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
+        // per-cell fallback: the cold ε ladder, every phase saturating only the arcs
+        // that violate its ε (the converged cells' optimal flows stay untouched)
+        const long long sat_thr = phases == 1 && use_warm && !fb
+                                      ? warm_thr
+                                      : ((pr_failed || fb || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
         pr_failed = false;
         const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
         // walk slack > 1 only while a finer phase or price refinement still follows

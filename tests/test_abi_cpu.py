@@ -62,7 +62,7 @@ int main(void) {
   P(ks_delta, id); P(ks_delta, src); P(ks_delta, dst); P(ks_delta, low); P(ks_delta, cap);
   P(ks_delta, cost); P(ks_delta, old_cost); P(ks_delta, excess);
   P(ks_result, status); P(ks_result, sweeps); P(ks_result, ms_phase); P(ks_result, n_nodes);
-  P(ks_result, ms_gu_kernels); P(ks_result, rebuilt); P(ks_result, recoveries);
+  P(ks_result, ms_gu_kernels); P(ks_result, rebuilt); P(ks_result, recoveries); P(ks_result, cell_fallbacks);
   P(ks_opts, warm_start); P(ks_opts, walk_slack); P(ks_opts, fault_inject); P(ks_opts, walk_passes); P(ks_opts, tail_nodes); P(ks_opts, bf_bound); P(ks_opts, fwd_nodes); P(ks_opts, cell_nodes); P(ks_opts, warm_shift); P(ks_opts, warm_canon); P(ks_opts, reserved);
   P(ks_store_stats, superseded); P(ks_store_stats, residual_slots);
   P(ks_flow, flow);
@@ -94,7 +94,7 @@ def test_struct_layouts_match_bindings(tmp_path):
             key = f"{cname}.{f}"
             if key in out:
                 assert dt.fields[f][1] == out[key], key
-    for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels", "rebuilt", "recoveries"):
+    for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels", "rebuilt", "recoveries", "cell_fallbacks"):
         assert getattr(native.KsResult, f).offset == out[f"ks_result.{f}"], f
     for f in ("warm_start", "walk_slack", "fault_inject", "walk_passes", "tail_nodes", "bf_bound", "fwd_nodes",
               "cell_nodes", "warm_shift", "warm_canon", "reserved"):

@@ -124,3 +124,22 @@ def test_c_abi_layout_matches_python_sharding():
         for g in range(64):
             assert native.batch_owner(g, world) == batch.owner(g, world)
         assert native.load().ks_batch_slots(64, world) == batch.slots_per_rank(64, world)
+
+
+def test_gather_has_no_early_return_after_the_status_all_reduce():
+    """VERDICT r4 item 5 (structure): between the status all-reduce and the end of
+    the send/receive group, ks_batch_gather neither returns nor uses KB_HIP (which
+    returns): a failing rank must never leave its peers waiting in ncclSend."""
+    src = open(os.path.join(os.path.dirname(HERE), "ksched_amd", "csrc", "ks_batch.hip")).read()
+    body = src[src.index("int ks_batch_gather("):]
+    a = body.index("rccl().AllReduce(")
+    g = body.index("const ncclResult_t ge = rccl().GroupEnd();", body.index("// 3. one group"))
+    seg = body[a:g]
+    # the only exits in between: the all-reduce's own error (after its GroupEnd) and
+    # the agreed error of every rank (the all-reduce's result), both before any send
+    exits = [ln.strip() for ln in seg.splitlines()
+             if ("return" in ln or "KB_HIP" in ln) and not ln.strip().startswith("//")]
+    assert not any("KB_HIP" in e for e in exits), exits
+    send = seg.index("// 3. one group")
+    assert all(seg.index(e) < send for e in exits), exits
+    assert "hipMalloc" not in seg[send:] and "KB_TRY" not in seg[send:]

@@ -227,6 +227,35 @@ def test_config5_cells_one_workgroup_each_vs_goldens():
         b.close()
 
 
+def test_failing_cell_falls_back_alone():
+    """a cell that gives up in the cell solver (injected: ks_opts
+    fault_inject bit 4 stops the middle cell of the batch after 40 operations with
+    CS_NOCONV) is re-solved on the multi-kernel engine; the other cells' optima are
+    kept, the solve returns KS_OK, and every cell equals the CPU oracle."""
+    graphs = [gen.quincy(2_000, 200, 10, 20, 1500 + i) for i in range(6)]
+    want = [ko.cost_scaling(g)[1:3] for g in graphs]
+    b = native.Batch(devices=[0], fault_inject=16)
+    try:
+        b.load(graphs)
+        res = b.solve()
+        assert res[0].raw["solver"] == 1 and res[0].raw["cells"] == 6
+        assert res[0].raw["cell_fallbacks"] == 1
+        pu, cost, flow = b.gather(2_000)
+        assert list(zip(cost.tolist(), flow.tolist())) == want
+        for i in (2, 3):
+            g = graphs[i]
+            tasks = np.nonzero(g.ntype == 1)[0] + 1
+            check_mapping(g, {int(t): int(p) for t, p in zip(tasks, pu[i]) if p})
+        # the next solve of the same batch runs in the cell solver again (no fault on
+        # a re-solve: the fault hits the first attempt of each solve the same way)
+        res = b.solve()
+        assert res[0].raw["cell_fallbacks"] == 1
+        _, cost2, _ = b.gather(2_000)
+        assert cost2.tolist() == cost.tolist()
+    finally:
+        b.close()
+
+
 def test_batch_gather_pack_failure_returns_error():
     """ADVICE / VERDICT r3: a rank whose packing fails (here: injected, ks_opts
     fault_inject bit 2, global rank 0) still reaches the collective point and
@@ -240,6 +269,23 @@ def test_batch_gather_pack_failure_returns_error():
             b.gather(1_000)
         assert ei.value.code == native.KS_E_DEVICE
         assert "injected pack failure" in str(ei.value)
+    finally:
+        b.close()
+
+
+def test_batch_gather_root_buffer_failure_returns_error():
+    """rank 0's receive buffer is allocated while packing (step 1),
+    so its failure (injected, ks_opts fault_inject bit 3) is a status word like any
+    other: the gather returns the error, and a later gather without the fault works."""
+    graphs = [gen.quincy(1_000, 100, 5, 10, 1400 + i) for i in range(3)]
+    b = native.Batch(devices=[0], fault_inject=8)
+    try:
+        b.load(graphs)
+        b.solve()
+        with pytest.raises(native.KsError) as ei:
+            b.gather(1_000)
+        assert ei.value.code == native.KS_E_DEVICE
+        assert "root buffer" in str(ei.value)
     finally:
         b.close()
 

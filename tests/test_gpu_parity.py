@@ -374,3 +374,33 @@ def test_failed_load_leaves_the_context_usable(ctx):
     r = ctx.solve()
     assert (r.cost, r.flow) == (c, fv)
     check_mapping(g, ctx.task_mapping())
+
+
+def test_cell_range_fallback_on_a_warm_start():
+    """a warm solve whose new costs no longer fit the cell solver's
+    compact record (scaled cost · (n+1) beyond int32) falls back to the engine; the
+    warm start's price shift is applied once, and the result equals the oracle's,
+    then and on the next warm solve."""
+    g = gen.quincy(1_000, 100, 5, 10, 31)          # 1,217 nodes: the cell solver by default
+    with native.Context(0, warm_start=1) as ctx:
+        ctx.load_graph(g)
+        r0 = ctx.solve()
+        assert r0.raw["solver"] == 1
+        assert (r0.cost, r0.flow) == ko.cost_scaling(g)[1:3]
+        src, dst, cost = g.src.tolist(), g.dst.tolist(), g.cost.tolist()
+        big = 3_000_000                            # × 1,218 > 2^31
+        d = np.zeros(50, native.DELTA_DT)
+        upd = {}
+        for k, i in enumerate(range(0, 5 * 50, 5)):   # task → U arcs (ageing)
+            d[k]["kind"], d[k]["src"], d[k]["dst"], d[k]["cap"] = native.KS_UPDATE_ARC, src[i], dst[i], 1
+            d[k]["cost"], d[k]["old_cost"] = cost[i] + big, cost[i]
+            upd[i] = cost[i] + big
+        ctx.apply_deltas(d)
+        h = gen.Graph(g.ntype, g.supply, g.src, g.dst, g.low, g.cap,
+                      np.asarray([upd.get(i, c) for i, c in enumerate(cost)], np.int64))
+        want = ko.cost_scaling(h)[1:3]
+        r1 = ctx.solve()
+        assert r1.raw["solver"] == 0 and r1.raw["warm_started"] == 1
+        assert (r1.cost, r1.flow) == want
+        r2 = ctx.solve()
+        assert (r2.cost, r2.flow) == want
