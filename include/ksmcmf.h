@@ -64,9 +64,11 @@
 extern "C" {
 #endif
 
-#define KSMCMF_ABI_VERSION 3   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls;
+#define KSMCMF_ABI_VERSION 4   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls;
                                   3: ks_opts.cell_nodes, ks_result per-kind timing and cell-solver
-                                  fields. ks_opts (96 B) and ks_result (320 B) CHANGED SIZE in
+                                  fields; 4: ks_opts.compact_pos (the last reserved word),
+                                  ks_result.cell_fallbacks (a reserved word), sizes unchanged.
+                                  ks_opts (96 B) and ks_result (320 B) CHANGED SIZE in
                                   ABI 2 and ks_result again in ABI 3: a caller must check
                                   ks_abi_version() == KSMCMF_ABI_VERSION before ks_create. */
 
@@ -158,7 +160,10 @@ typedef struct ks_opts {
                                   d = p), so carried prices do not drift [0: on]; < 0 off.
                                   Multi-kernel engine only: a cell-solver solve keeps the
                                   prices its workgroup ended with                      */
-    int32_t  reserved[1];
+    int32_t  compact_pos;      /* the multi-kernel engine's solve reads 16-byte residual
+                                  records (32-bit residual, pair capacity, scaled cost,
+                                  head) when every scaled cost and capacity fits, else
+                                  the 32-byte ones [0: on]; < 0: always 32-byte (ABI 4)  */
 } ks_opts;
 
 typedef struct ks_node {       /* one "n id excess type" line                            */
@@ -233,7 +238,7 @@ typedef struct ks_result {
     double   ms_fs_kernels;    /* event-timed span of the forward-update batches (ms)   */
     uint64_t fwd_updates;      /* forward tail updates completed                        */
     int32_t  cells;            /* cells the cell solver ran (one workgroup each)        */
-    int32_t  _pad3;
+    int32_t  compact;          /* 1: the engine's solve read 16-byte residual records   */
     double   ms_cell_kernel;   /* event-timed duration of the cell-solver launches (ms) */
     uint64_t cell_ticks_max;   /* slowest cell's in-kernel solve time (100 MHz ticks)   */
     uint64_t cell_ticks_sum;   /* Σ over cells of their in-kernel solve times            */

@@ -114,6 +114,7 @@ struct Ctl {
     int infeasible;
     int bf_done;           // Bellman-Ford frontier drained (update converged)
     int verify_bad;
+    int cp_bad;            // k_pack_pos: a value the 16-B record cannot hold (the solve reads Pos)
     int bf_count;          // Bellman-Ford rounds that did work (whole solve)
     int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
     int apply_act;         // the global-update apply seeded a non-empty frontier
@@ -179,6 +180,8 @@ struct DG {
     int expand;            // Bellman-Ford: relax low-degree targets two hops per round
     const int* first;
     Pos* pos;              // residual positions: cost, rcap, ucap = rcap(a) + rcap(rev a), head, rev
+    CPos* cp;              // compact solve: 16-B copies of the positions (nullptr: the solve reads pos)
+    int* crev;             // compact solve: reverse position of each position
     long long* excess;
     long long* p0;         // node records (stride 4, index with ni()): p0 at +0, dist at +1, p1 at +2
     long long* p1;
@@ -274,6 +277,69 @@ __device__ __forceinline__ Pos ld_pos(const Pos* p) {
     return r;
 }
 
+// Position access of the solve's hot kernels, by record layout:
+// PL<false> reads the 32-B Pos records, PL<true> the 16-B CPos copies (32-bit
+// residual, pair capacity, scaled cost, head) plus the separate reverse array.
+// Every hot kernel is instantiated for both; the host launches the compact one when
+// the graph's scaled costs and capacities fit 32 bits (ks_opts.compact_pos).
+template <bool CP>
+struct PL;
+template <>
+struct PL<false> {
+    static __device__ __forceinline__ Pos ld(const DG& g, int a) { return ld_pos(g.pos + a); }
+    // the record without its reverse position (Bellman-Ford): the same loads here
+    static __device__ __forceinline__ Pos ld_nr(const DG& g, int a) { return ld_pos(g.pos + a); }
+    static __device__ __forceinline__ void set_rc(const DG& g, int a, long long v) { g.pos[a].rcap = v; }
+    static __device__ __forceinline__ long long rc_atomic(const DG& g, int a) { return atom_load(&g.pos[a].rcap); }
+    static __device__ __forceinline__ bool cas_rc(const DG& g, int a, long long& exp, long long v) {
+        return __hip_atomic_compare_exchange_strong(&g.pos[a].rcap, &exp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    }
+    static __device__ __forceinline__ void add_rc(const DG& g, int a, long long v) { atom_add(&g.pos[a].rcap, v); }
+    static __device__ __forceinline__ int head(const DG& g, int a) { return g.pos[a].head; }
+    static __device__ __forceinline__ int rev(const DG& g, int a) { return g.pos[a].rev; }
+};
+template <>
+struct PL<true> {
+    static __device__ __forceinline__ Pos ld(const DG& g, int a) {
+        const int4 w = reinterpret_cast<const int4*>(g.cp)[a];
+        const int rv = g.crev[a];   // issued with the record (independent address)
+        Pos r;
+        r.rcap = w.x;
+        r.ucap = w.y;
+        r.cost = w.z;   // CPOS_DEAD for inert positions: never residual, reduced cost > ε
+        r.head = w.w;
+        r.rev = rv;
+        return r;
+    }
+    static __device__ __forceinline__ Pos ld_nr(const DG& g, int a) {
+        const int4 w = reinterpret_cast<const int4*>(g.cp)[a];
+        Pos r;
+        r.rcap = w.x;
+        r.ucap = w.y;
+        r.cost = w.z;
+        r.head = w.w;
+        r.rev = -1;
+        return r;
+    }
+    static __device__ __forceinline__ void set_rc(const DG& g, int a, long long v) { g.cp[a].rcap = (int)v; }
+    static __device__ __forceinline__ long long rc_atomic(const DG& g, int a) {
+        return __hip_atomic_load(&g.cp[a].rcap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    static __device__ __forceinline__ bool cas_rc(const DG& g, int a, long long& exp, long long v) {
+        int e = (int)exp;
+        const bool ok = __hip_atomic_compare_exchange_strong(&g.cp[a].rcap, &e, (int)v, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        exp = e;
+        return ok;
+    }
+    static __device__ __forceinline__ void add_rc(const DG& g, int a, long long v) {
+        __hip_atomic_fetch_add(&g.cp[a].rcap, (int)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    static __device__ __forceinline__ int head(const DG& g, int a) { return g.cp[a].head; }
+    static __device__ __forceinline__ int rev(const DG& g, int a) { return g.crev[a]; }
+};
+
 // ------------------------------------------------------------ wave helpers ---
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 __device__ __forceinline__ long long wave_sum(long long x) {
@@ -364,14 +430,11 @@ __device__ __forceinline__ void flush_counters(const DG& g, const Cnt& c) {
 // and flagged once per wave in flush_pending.
 // rv / uc: the arc's reverse position and pair capacity when the caller loaded
 // them with the arc (rv < 0: load them here, one more dependent step).
+template <bool CP>
 __device__ __forceinline__ void push_arc(const DG& g, const Front* nf, int a, int w, long long r, long long d,
-                                         Pend& pd, int& out, int rv = -1, long long uc = 0) {
-    if (rv < 0) {
-        rv = g.pos[a].rev;
-        uc = g.pos[a].ucap;
-    }
-    g.pos[a].rcap = r - d;
-    g.pos[rv].rcap = uc - (r - d);
+                                         Pend& pd, int& out, int rv, long long uc) {
+    PL<CP>::set_rc(g, a, r - d);
+    PL<CP>::set_rc(g, rv, uc - (r - d));
     if (w < g.hub_base) {
         atom_add(&g.excess[w], d);
         if (nf) {
@@ -720,6 +783,33 @@ __global__ void k_max_cost(int hi, const unsigned char* __restrict__ alive, cons
     }
 }
 
+// The compact solve (ks_opts.compact_pos): every position's 16-B copy
+// and its reverse before the phases; a value a 32-bit field cannot hold sets *bad
+// and the solve reads the 32-B records instead. The residuals go back before
+// verification (k_unpack_pos).
+__global__ void k_pack_pos(long long m2, const Pos* __restrict__ pos, CPos* __restrict__ cp, int* __restrict__ crev,
+                           int* __restrict__ bad) {
+    int b = 0;
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK) {
+        const Pos q = ld_pos(pos + p);
+        const bool dead = q.cost >= DEAD_COST;
+        b |= (!dead && (q.cost > CPOS_MAX || q.cost < -CPOS_MAX)) || q.rcap < 0 || q.rcap > CPOS_MAX || q.ucap < 0 ||
+             q.ucap > CPOS_MAX;
+        int4 w;
+        w.x = (int)q.rcap;
+        w.y = (int)q.ucap;
+        w.z = dead ? CPOS_DEAD : (int)q.cost;
+        w.w = q.head;
+        reinterpret_cast<int4*>(cp)[p] = w;
+        crev[p] = q.rev;
+    }
+    if (__any(b) && lane_id() == 0) atomicOr(bad, 1);
+}
+__global__ void k_unpack_pos(long long m2, const CPos* __restrict__ cp, Pos* __restrict__ pos) {
+    for (long long p = blockIdx.x * (long long)BLK + threadIdx.x; p < m2; p += (long long)gridDim.x * BLK)
+        pos[p].rcap = cp[p].rcap;
+}
+
 struct ClassIs {
     const unsigned char* cls;
     unsigned char c;
@@ -729,7 +819,7 @@ struct ClassIs {
 // ================================================= saturate (phase start) ===
 // Push the full residual capacity of every arc with negative reduced cost
 // (Goldberg's refine start) over the whole graph; reads the authoritative p0.
-template <int G>
+template <int G, bool CP>
 __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pend& pd, int& out, Cnt& c) {
     const long long* P = g.p0;
     const int lig = lane_id() & (G - 1);
@@ -744,12 +834,12 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            const Pos q = ld_pos(g.pos + a);
+            const Pos q = PL<CP>::ld(g, a);
             const long long r = q.rcap;
             if (r > 0) {
                 const int w = q.head;
                 if (q.cost + pv - P[ni(w)] < -thr) {
-                    push_arc(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
+                    push_arc<CP>(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
                     tot += r;
                     c.push++;
                 }
@@ -763,6 +853,7 @@ __device__ __forceinline__ void sat_group(const DG& g, int v, long long thr, Pen
 
 // thr = 0: Goldberg's refine start (every negative reduced cost); thr = ε on a
 // warm start: only arcs that violate ε-optimality are saturated.
+template <bool CP>
 __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
     const long long* P = g.p0;
     Pend pd{-1, 0};
@@ -777,12 +868,12 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
         for (int k = 0; k < PER_T; ++k) {
             const int a = it.begin + threadIdx.x * PER_T + k;
             if (a < it.end) {
-                const Pos q = ld_pos(g.pos + a);
+                const Pos q = PL<CP>::ld(g, a);
                 const long long r = q.rcap;
                 if (r > 0) {
                     const int w = q.head;
                     if (q.cost + px - P[ni(w)] < -thr) {
-                        push_arc(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
+                        push_arc<CP>(g, nullptr, a, w, r, r, pd, out, q.rev, q.ucap);
                         tot += r;
                         c.push++;
                     }
@@ -796,7 +887,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
         return;
     }
     const Scan sc{nullptr, 1};
-#define KS_SAT_CALL(C) sat_group<G_>(g, v, thr, pd, out, c)
+#define KS_SAT_CALL(C) sat_group<G_, CP>(g, v, thr, pd, out, c)
     KS_BY_CLASS(wave_index_in_grid(g.nhitems), sc, KS_SAT_CALL)
 #undef KS_SAT_CALL
     flush_pending(g, nullptr, pd, out);
@@ -806,7 +897,7 @@ __global__ __launch_bounds__(BLK) void k_saturate(DG g, long long thr) {
 // =================================================== push/relabel sweep ===
 // One node per G-lane group, one residual arc per lane; admissible capacity is
 // distributed by an in-group prefix sum, the relabel minimum by a group min.
-template <int G>
+template <int G, bool CP>
 __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v, long long e, long long pv, int b0,
                                             int en, long long* __restrict__ PN, const long long* __restrict__ P,
                                             long long eps, Pend& pd, int& out, Cnt& c) {
@@ -825,7 +916,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         int rv = 0;
         long long uc = 0;
         if (valid) {
-            const Pos q = ld_pos(g.pos + a);   // the whole record: a push needs no further load
+            const Pos q = PL<CP>::ld(g, a);   // the whole record: a push needs no further load
             r = q.rcap;
             w = q.head;
             rv = q.rev;
@@ -839,7 +930,7 @@ __device__ __forceinline__ void sweep_group(const DG& g, const Front& nf, int v,
         long long d = rem - (incl - adm);
         d = d < 0 ? 0 : (d > adm ? adm : d);
         if (d > 0) {
-            push_arc(g, &nf, a, w, r, d, pd, out, rv, uc);
+            push_arc<CP>(g, &nf, a, w, r, d, pd, out, rv, uc);
             c.push++;
         }
         if (valid) {
@@ -923,6 +1014,7 @@ __device__ __forceinline__ void settle(const DG& g, const Front& F, const Front&
 
 // Hub chunk: one workgroup, 1024 arcs (four per thread, loads issued together).
 // px, E: the hub's price and excess, loaded by the caller with its flag.
+template <bool CP>
 __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HItem& it, long long px, long long E,
                           const long long* __restrict__ P, long long* __restrict__ PN, long long eps, Pend& pd,
                           int& out, Cnt& c) {
@@ -941,7 +1033,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
         uc[k] = 0;
         cr[k] = 0;
         if (a < it.end) {
-            const Pos q = ld_pos(g.pos + a);
+            const Pos q = PL<CP>::ld(g, a);
             r[k] = q.rcap;
             w[k] = q.head;
             rv[k] = q.rev;
@@ -973,7 +1065,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
         const long long d = adm[k] < rt ? adm[k] : rt;
         rt -= d;
         if (d > 0) {
-            push_arc(g, &N, a, w[k], r[k], d, pd, out, rv[k], uc[k]);
+            push_arc<CP>(g, &N, a, w[k], r[k], d, pd, out, rv[k], uc[k]);
             c.push++;
         }
         if (a < it.end) {
@@ -1004,6 +1096,7 @@ __device__ void hub_chunk(const DG& g, const Front& F, const Front& N, const HIt
 // by one block-wide scan. A rack (≈ 440 arcs) is one pass — with one wave per
 // node it took two dependent batches, and the chunked node was the last block
 // of almost every sweep (round 3's per-launch block stamps).
+template <bool CP>
 __device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, int x, long long e, long long px,
                                    int b0, int en, long long* __restrict__ PN, const long long* __restrict__ P,
                                    long long eps, Pend& pd, int& out, Cnt& c) {
@@ -1024,7 +1117,7 @@ __device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, 
             rv[j] = 0;
             uc[j] = 0;
             if (a < en) {
-                const Pos q = ld_pos(g.pos + a);
+                const Pos q = PL<CP>::ld(g, a);
                 r[j] = q.rcap;
                 w[j] = q.head;
                 cs[j] = q.cost;
@@ -1052,7 +1145,7 @@ __device__ void node_discharge_blk(const DG& g, const Front& F, const Front& N, 
             d = d < 0 ? 0 : d;
             avail -= d;
             if (d > 0) {
-                push_arc(g, &N, a, w[j], r[j], d, pd, out, rv[j], uc[j]);
+                push_arc<CP>(g, &N, a, w[j], r[j], d, pd, out, rv[j], uc[j]);
                 c.push++;
             }
             if (a < en) {
@@ -1165,7 +1258,7 @@ __device__ __forceinline__ void window_node(const WinFlag& f, int v, int base, l
 // otherwise test the words first, or sink the other loads under the test).
 #define KS_AFTER_LOADS(c0, c1, ...) asm volatile("" : "+v"(c0), "+v"(c1) : __VA_ARGS__)
 
-template <int C>
+template <int C, bool CP>
 __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, unsigned long long mask,
                                           const WinFlag& f, const long long* __restrict__ P,
                                           long long* __restrict__ PN, long long eps, Pend& pd, int& out, Cnt& c) {
@@ -1182,12 +1275,13 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
         int b0 = 0, en = 0;
         window_node(f, v, base, e, pv, b0, en);
         if (v < 0) e = 0;
-        sweep_group<G>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
+        sweep_group<G, CP>(g, N, v, e, pv, b0, en, PN, P, eps, pd, out, c);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
 }
 
 
+template <bool CP>
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
@@ -1215,7 +1309,7 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
         ctl_words();
         KS_AFTER_LOADS(c_done, c_act, "v"(fl), "v"(px), "v"(E));
         if (c_done && c_act && fl) {
-            hub_chunk(g, F, N, it, px, E, P, PN, eps, pd, out, c);
+            hub_chunk<CP>(g, F, N, it, px, E, P, PN, eps, pd, out, c);
         }
     } else if ((int)blockIdx.x >= g.nhitems + g.sw_clsb) {
         // chunked class: one workgroup per node (a wave per node made the chunked
@@ -1242,7 +1336,7 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             }
             __syncthreads();
             if (s_go) {
-                node_discharge_blk(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
+                node_discharge_blk<CP>(g, F, N, x, s_e, px, b0, en, PN, P, eps, pd, out, c);
             }
         }
     } else {
@@ -1268,11 +1362,11 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
             switch (class_of_window(g, w)) {
-                case 0: sweep_win<0>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
-                case 1: sweep_win<1>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
-                case 2: sweep_win<2>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
-                case 3: sweep_win<3>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
-                default: sweep_win<4>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 0: sweep_win<0, CP>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 1: sweep_win<1, CP>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 2: sweep_win<2, CP>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                case 3: sweep_win<3, CP>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
+                default: sweep_win<4, CP>(g, N, w, mk[j], wf[j], P, PN, eps, pd, out, c); break;
             }
         }
     }
@@ -1319,7 +1413,7 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 
 // Relax the in-arcs of a low-degree node u (≤ 8 arcs: tasks, PUs) right after
 // its distance dropped to du: a second hop inside the same round.
-template <bool PR>
+template <bool PR, bool CP>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
                                             int b0, int b1, long long eps, long long B, long long* hub_min, int& out) {
     // the records of all (≤ 8) arcs issued together; usually one in-arc carries
@@ -1332,21 +1426,23 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         hd[k] = 0;
         cb[k] = 0;
         if (b0 + k < b1) {
-            const Pos q = ld_pos(g.pos + b0 + k);
+            const Pos q = PL<CP>::ld_nr(g, b0 + k);
             hd[k] = q.head;
             cb[k] = q.cost;
             if (q.ucap - q.rcap > 0) live |= 1u << k;
         }
     }
-    for (int b = b1 - b0 > 8 ? b0 + 8 : b1; b < b1; ++b)   // leaves have ≤ 8 arcs; kept for safety
-        if (g.pos[b].ucap - g.pos[b].rcap > 0) {
-            const int u2 = g.pos[b].head;
-            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], g.pos[b].cost, pu, eps);
+    for (int b = b1 - b0 > 8 ? b0 + 8 : b1; b < b1; ++b) {   // leaves have ≤ 8 arcs; kept for safety
+        const Pos q = PL<CP>::ld_nr(g, b);
+        if (q.ucap - q.rcap > 0) {
+            const int u2 = q.head;
+            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], q.cost, pu, eps);
             if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, B, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
             }
         }
+    }
     while (live) {
         const int k = __builtin_ctz(live);
         live &= live - 1;
@@ -1370,10 +1466,10 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
 
 // Relax in-arc (u→v) = reverse of CSR arc a = (v→u); residual ucap − rcap,
 // cost −cost(a). Loads are issued before the residual test (short chain).
-template <bool PR>
+template <bool PR, bool CP>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
                                          long long eps, long long B, long long* hub_min, int& out) {
-    const Pos q = ld_pos(g.pos + a);
+    const Pos q = PL<CP>::ld_nr(g, a);
     const long long rin = q.ucap - q.rcap;
     // an arc that cannot relax reads node 0's (hot) record instead of its head's
     // random line: the loads stay unconditional (no branch join to wait at) and
@@ -1389,14 +1485,14 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
     if (!offer<PR>(g, nf, u, cand, du, B, hub_min, out)) return;
     if (leaf) {
-        expand_leaf<PR>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
+        expand_leaf<PR, CP>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
     } else {
         nf.flag[u] = 1;
         out = 1;
     }
 }
 
-template <int G, bool PR>
+template <int G, bool PR, bool CP>
 __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v, long long dv, long long pv, int b0,
                                              int en, long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
@@ -1406,14 +1502,14 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR>(g, nf, a, dv, pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, a, dv, pv, eps, B, hub_min, out);
             scans++;
         }
     }
 }
 
 // Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
-template <int C, bool PR>
+template <int C, bool PR, bool CP>
 __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, const WinFlag& f,
                                        long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     constexpr int G = class_lanes(C);
@@ -1429,25 +1525,25 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         int b0 = 0, en = 0;
         window_node(f, v, base, d, pv, b0, en);
         if (v < 0) d = INF64;
-        bf_group_pre<G, PR>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans);
+        bf_group_pre<G, PR, CP>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
 }
 
 // One 64-arc chunk of a chunked-class node (its flag already tested).
-template <bool PR>
+template <bool PR, bool CP>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
                                          long long B, long long* hub_min, int& out, long long& scans) {
     const long long dv = atom_load(&g.dist[ni(ci.node)]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
-        relax_in<PR>(g, N, a, dv, g.p0[ni(ci.node)], eps, B, hub_min, out);
+        relax_in<PR, CP>(g, N, a, dv, g.p0[ni(ci.node)], eps, B, hub_min, out);
         scans++;
     }
 }
 
-template <int G, bool PR>
+template <int G, bool PR, bool CP>
 __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long B, long long* hub_min,
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
@@ -1464,7 +1560,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR>(g, nf, a, dv, pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, a, dv, pv, eps, B, hub_min, out);
             scans++;
         }
     }
@@ -1473,7 +1569,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
 // One Bellman-Ford round. dense = 1: every node (first round of an update).
 // dense_arg < 0: the round is dense iff it is the running update's first
 // (bf_seq0, set by the init kernel); ≥ 0: as given.
-template <bool PR>
+template <bool PR, bool CP>
 __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) {
     const int dense = dense_arg >= 0 ? dense_arg : (seq == g.ctl->bf_seq0 ? 1 : 0);
     __shared__ long long hub_min[HUB_LDS];
@@ -1516,7 +1612,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR>(g, N, a, dv, pv, eps, B, hub_min, out);
+                        relax_in<PR, CP>(g, N, a, dv, pv, eps, B, hub_min, out);
                         scans++;
                     }
                 }
@@ -1529,11 +1625,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             // the update already converged
         } else if (w < g.wbeg[CCLS]) {
             const Scan sc{F.flag, 1};
-#define KS_BF_CALL(C) bf_group<G_, PR>(g, N, v, eps, B, hub_min, out, scans)
+#define KS_BF_CALL(C) bf_group<G_, PR, CP>(g, N, v, eps, B, hub_min, out, scans)
             KS_BY_CLASS(w, sc, KS_BF_CALL)
 #undef KS_BF_CALL
         } else if (w - g.wbeg[CCLS] < g.ncitems) {
-            bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
+            bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
         }
     } else {
         const int tw = ((int)gridDim.x - nhb) * WPB;
@@ -1565,15 +1661,15 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
-                bf_chunk<PR>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
+                bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
                 continue;
             }
             switch (class_of_window(g, w)) {
-                case 0: bf_win<0, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 1: bf_win<1, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 2: bf_win<2, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 3: bf_win<3, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                default: bf_win<4, PR>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 0: bf_win<0, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 1: bf_win<1, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 2: bf_win<2, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 3: bf_win<3, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                default: bf_win<4, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
             }
         }
     }
@@ -1861,6 +1957,7 @@ constexpr int AUG_STEPS = 512;     // hops per walk before its units are left wh
 // hands it to its qualifying arcs, one workgroup per chunk claiming its share
 // with one returning atomic (as the sweeps' hub chunks do); the fed nodes are
 // listed for the second walker pass.
+template <bool CP>
 __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
     __shared__ long long sh[WPB];
     __shared__ long long s_take;
@@ -1887,8 +1984,8 @@ __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
         uc[k] = 0;
         adm[k] = 0;
         if (a < it.end) {
-            const Pos q = ld_pos(g.pos + a);
-            r[k] = atom_load(&g.pos[a].rcap);   // the first walker pass claimed with atomics
+            const Pos q = PL<CP>::ld(g, a);
+            r[k] = PL<CP>::rc_atomic(g, a);   // the first walker pass claimed with atomics
             w[k] = q.head;
             rv[k] = q.rev;
             uc[k] = q.ucap;
@@ -1922,8 +2019,8 @@ __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
         rt -= d;
         if (d <= 0) continue;
         const int a = it.begin + threadIdx.x * PER_T + k;
-        g.pos[a].rcap = r[k] - d;              // only this chunk touches the pair in this kernel
-        g.pos[rv[k]].rcap = uc[k] - (r[k] - d);
+        PL<CP>::set_rc(g, a, r[k] - d);   // only this chunk touches the pair in this kernel
+        PL<CP>::set_rc(g, rv[k], uc[k] - (r[k] - d));
         const long long now = atom_add_ret(&g.excess[w[k]], d) + d;
         if (now > 0) {
             mark(g, F, w[k], dummy);
@@ -1935,6 +2032,7 @@ __global__ __launch_bounds__(BLK) void k_aug_hub(DG g, int sseq, int slack) {
 
 // mode 0: from the apply's excess nodes (non-hubs); mode 1: from the nodes a hub
 // distribution (k_aug_hub) fed.
+template <bool CP>
 __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int slack) {
     if (!g.ctl->bf_done) return;
     const int nx = g.ctl->n_exc;
@@ -1966,8 +2064,8 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
             const int a = base + lane;
             long long key = INF64;
             if (a < en) {
-                const Pos q = ld_pos(g.pos + a);
-                const long long r = atom_load(&g.pos[a].rcap);   // other walkers claim with atomics
+                const Pos q = PL<CP>::ld_nr(g, a);
+                const long long r = PL<CP>::rc_atomic(g, a);   // other walkers claim with atomics
                 const long long cr = q.cost + pu - g.p0[ni(q.head)];
                 const long long dw = atom_load(&g.dist[ni(q.head)]);
                 if (r > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
@@ -1984,8 +2082,8 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
         long long take = 0;
         int w = 0;
         if (lane == 0) {
-            w = g.pos[ba].head;
-            long long r = atom_load(&g.pos[ba].rcap);
+            w = PL<CP>::head(g, ba);
+            long long r = PL<CP>::rc_atomic(g, ba);
             for (;;) {
                 take = r < carry ? r : carry;
                 if (take <= 0) {
@@ -1993,12 +2091,10 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
                     break;
                 }
                 long long exp = r;
-                if (__hip_atomic_compare_exchange_strong(&g.pos[ba].rcap, &exp, r - take, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    break;
+                if (PL<CP>::cas_rc(g, ba, exp, r - take)) break;
                 r = exp;
             }
-            if (take > 0) atom_add(&g.pos[g.pos[ba].rev].rcap, take);
+            if (take > 0) PL<CP>::add_rc(g, PL<CP>::rev(g, ba), take);
             if (take < carry) {   // the rest stays at u
                 atom_add(&g.excess[u], carry - take);
                 mark(g, F, u, dummy);
@@ -2112,9 +2208,10 @@ __global__ void k_fs_init(DG g, int seq0) {
 
 // Relax residual out-arc a of u (distance du, price pu). Returns 1 when a
 // non-hub, non-deficit head w was lowered and is not yet listed for the next round.
+template <bool CP>
 __device__ __forceinline__ int fs_relax(const DG& g, const Front& N, int a, long long du, long long pu, long long eps,
                                         long long B, int& wout) {
-    const Pos q = ld_pos(g.pos + a);
+    const Pos q = PL<CP>::ld_nr(g, a);
     const int w = q.head;
     const long long pw = g.p0[ni(w)];
     const long long kw = atom_load(&g.dist[ni(w)]);
@@ -2142,6 +2239,7 @@ __device__ __forceinline__ int fs_relax(const DG& g, const Front& N, int a, long
 
 // One round: the listed nodes (one wave per node, 64 arcs per batch) and the
 // flagged hubs (HSPLIT workgroups per 1024-arc chunk) relax their out-arcs.
+template <bool CP>
 __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
     const int lin = seq % 3, lout = (seq + 1) % 3;
     const Front F = g.bf[lin], N = g.bf[lout];
@@ -2188,7 +2286,7 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
         for (int k = 0; k < BF_PER_T; ++k) {
             const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
             int w = -1;
-            const int add = a < it.end ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            const int add = a < it.end ? fs_relax<CP>(g, N, a, du, pu, eps, B, w) : 0;
             scans += a < it.end;
             fs_append(g, lout, add, w);
         }
@@ -2212,7 +2310,7 @@ __global__ __launch_bounds__(BLK) void k_fs_round(DG g, int seq) {
         for (int base = b0; base < b1; base += WAVE) {
             const int a = base + lane;
             int w = -1;
-            const int add = a < b1 ? fs_relax(g, N, a, du, pu, eps, B, w) : 0;
+            const int add = a < b1 ? fs_relax<CP>(g, N, a, du, pu, eps, B, w) : 0;
             scans += a < b1;
             fs_append(g, lout, add, w);
         }
@@ -2257,6 +2355,7 @@ __global__ void k_fs_apply(DG g) {
 // (another wave took it) every claim is rolled back and the unit waits for the
 // next update. Then the reverse residuals and the deficit are credited.
 constexpr int FS_PATH = 512;       // hops a trace may take
+template <bool CP>
 __global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
     __shared__ int path[FS_PATH];
     __shared__ int s_len, s_src;
@@ -2276,9 +2375,9 @@ __global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
                 break;
             }
             if (a >= g.npos) break;   // (a key not written by this search)
-            const Pos q = ld_pos(g.pos + a);
-            const long long r = atom_load(&g.pos[a].rcap);
-            const int u = g.pos[q.rev].head;
+            const Pos q = PL<CP>::ld(g, (int)a);
+            const long long r = PL<CP>::rc_atomic(g, (int)a);
+            const int u = PL<CP>::head(g, q.rev);
             if (q.head != v || r <= 0 || q.cost + g.p0[ni(u)] - g.p0[ni(v)] >= 0) break;
             amt = r < amt ? r : amt;
             path[len++] = (int)a;
@@ -2315,16 +2414,14 @@ __global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
     bool ok = true;
     unsigned long long mine = 0;   // bit i: this lane holds the claim on path[lane + 64 i]
     for (int i = lane, k = 0; i < len; i += WAVE, ++k) {
-        long long* rc = &g.pos[path[i]].rcap;
-        long long r = atom_load(rc);
+        long long r = PL<CP>::rc_atomic(g, path[i]);
         for (;;) {
             if (r < amt) {
                 ok = false;
                 break;
             }
             long long exp = r;
-            if (__hip_atomic_compare_exchange_strong(rc, &exp, r - amt, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+            if (PL<CP>::cas_rc(g, path[i], exp, r - amt)) {
                 mine |= 1ULL << k;
                 break;
             }
@@ -2334,8 +2431,8 @@ __global__ __launch_bounds__(WAVE) void k_fs_trace(DG g) {
     const bool all = __all(ok);
     for (int i = lane, k = 0; i < len; i += WAVE, ++k) {
         if (!(mine >> k & 1)) continue;
-        if (all) atom_add(&g.pos[g.pos[path[i]].rev].rcap, amt);
-        else atom_add(&g.pos[path[i]].rcap, amt);   // roll back
+        if (all) PL<CP>::add_rc(g, PL<CP>::rev(g, path[i]), amt);
+        else PL<CP>::add_rc(g, path[i], amt);   // roll back
     }
     if (lane == 0) {
         if (all) {
@@ -2806,6 +2903,8 @@ struct EngineImpl {
     int64_t m2cap = 0;        // residual positions (Σ segment capacities)
     DBuf<int> first, ent, used, scur, perm, iperm;
     DBuf<Pos> pos;
+    DBuf<CPos> cpos;               // the compact solve's 16-B positions (k_pack_pos)
+    DBuf<int> crev;
     DBuf<long long> excess;
     DBuf<long long> nd;            // node records [p0, dist, p1, pad] × nn
     DBuf<unsigned> keys_in, keys_out;
@@ -2901,7 +3000,7 @@ struct EngineImpl {
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
         first.release(); pos.release(); ent.release(); used.release(); scur.release(); perm.release(); iperm.release();
-        excess.release(); nd.release();
+        excess.release(); nd.release(); cpos.release(); crev.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
@@ -3043,6 +3142,13 @@ struct EngineImpl {
             err = std::string(#expr) + ": " + hipGetErrorString(_e);     \
             return KS_E_DEVICE;                                          \
         }                                                                \
+    } while (0)
+
+// A hot kernel of the solve in the record layout the solve reads.
+#define KS_HOT(CPV, K, GRID, BLKS, ST, ...)                                                     \
+    do {                                                                                        \
+        if (CPV) K<true><<<dim3(GRID), dim3(BLKS), 0, ST>>>(__VA_ARGS__);                      \
+        else K<false><<<dim3(GRID), dim3(BLKS), 0, ST>>>(__VA_ARGS__);                         \
     } while (0)
 
 Engine::Engine() : p_(new EngineImpl) {}
@@ -4042,9 +4148,21 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     if (hi)
         hipLaunchKernelGGL(k_max_cost, dim3(grid_for(hi, 512)), dim3(BLK), 0, st, hi,
                            (const unsigned char*)s.a_alive.p, (const long long*)s.a_cost.p, &s.ctl.p->gu_L);
+    // the engine's hot kernels read 16-B copies of the positions when every value
+    // fits; the range flag comes back with the control block below
+    const bool want_cp = !s.cell_layout && s.opts.compact_pos >= 0 && m2 > 0;
+    if (want_cp) {
+        KS_CHECK(s.cpos.ensure(m2));
+        KS_CHECK(s.crev.ensure(m2));
+        hipLaunchKernelGGL(k_pack_pos, dim3(grid_for(m2, 4096)), dim3(BLK), 0, st, (long long)m2,
+                           (const Pos*)s.pos.p, s.cpos.p, s.crev.p, &s.ctl.p->cp_bad);
+    }
     KS_CHECK(hipMemcpyAsync(s.h_ctl, s.ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, st));
     KS_CHECK(hipStreamSynchronize(st));
     const long long maxc = s.h_ctl->gu_L;
+    const bool cpv = want_cp && !s.h_ctl->cp_bad;
+    bool cp_dirty = false;   // the compact residuals hold changes Pos does not have yet
+    res.compact = cpv ? 1 : 0;
     KS_CHECK(hipMemsetAsync(&s.ctl.p->gu_L, 0, sizeof(long long), st));
     const long long mult = s.mult;
     if (maxc > 0 && (double)maxc * (double)mult * 8.0 * (double)mult > 4.0e18) {
@@ -4058,6 +4176,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // the environment changes the algorithm.
     const ks_opts& o = s.opts;
     DG g = s.dg();
+    g.cp = cpv ? s.cpos.p : nullptr;
+    g.crev = cpv ? s.crev.p : nullptr;
     g.expand = o.two_hop < 0 ? 0 : 1;      // two hops per round through tasks and PUs
     g.bound = o.bf_bound < 0 ? 0 : 1;      // tail updates bounded at the excess nodes' distances
     g.fs_wide = std::max(2048, nn / 4);   // (measured: config 4's searches ≤ nn/6 wide, config 3's hub-bound ones ~nn/4 to 3nn/4)
@@ -4149,8 +4269,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         for (int r = 0; r < k; ++r) {
             const int dense = (first_dense && r == 0) ? 1 : 0;
             const int grid = dense ? dgrid : sgrid;
-            if (pr) hipLaunchKernelGGL(k_bf_round<true>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
-            else hipLaunchKernelGGL(k_bf_round<false>, dim3(grid), dim3(BLK), 0, st, g, bseq, dense);
+            if (pr) {
+                if (cpv) k_bf_round<true, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                else k_bf_round<true, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+            } else {
+                if (cpv) k_bf_round<false, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                else k_bf_round<false, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+            }
             ++bseq;
             ++bf_launches;
         }
@@ -4192,7 +4317,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl) -> int {
         KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
-        hipLaunchKernelGGL(k_saturate, dim3(fgrid), dim3(BLK), 0, st, g, sat_thr);
+        KS_HOT(cpv, k_saturate, fgrid, BLK, st, g, sat_thr);
+        cp_dirty = cpv;
         KS_CHECK(hipEventRecord(s.ev[3], st));
         uint64_t phase_sweeps = 0;
         int gi = gi_base;     // sweeps in the next cycle (fewer in a phase's tail, where walks augment)
@@ -4212,13 +4338,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 hipLaunchKernelGGL(k_fs_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq);
                 if ((e = hipEventRecord(s.fev[par][2 * u], st)) != hipSuccess) return e;
                 for (int r = 0; r < kf; ++r) {
-                    hipLaunchKernelGGL(k_fs_round, dim3(fsgrid), dim3(BLK), 0, st, g, bseq);
+                    KS_HOT(cpv, k_fs_round, fsgrid, BLK, st, g, bseq);
                     ++bseq;
                     ++fs_launches;
                 }
                 if ((e = hipEventRecord(s.fev[par][2 * u + 1], st)) != hipSuccess) return e;
                 hipLaunchKernelGGL(k_fs_apply, dim3(ngrid), dim3(BLK), 0, st, g);
-                hipLaunchKernelGGL(k_fs_trace, dim3(FDEF_CAP), dim3(WAVE), 0, st, g);
+                KS_HOT(cpv, k_fs_trace, FDEF_CAP, WAVE, st, g);
                 hipLaunchKernelGGL(k_fs_end, dim3(1), dim3(WAVE), 0, st, g);
             }
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 1);
@@ -4234,7 +4360,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipError_t e = hipEventRecord(s.cev[par][0], st);
             if (e != hipSuccess) return e;
             for (int r = 0; r < kb; ++r) {   // sparse from the first round: k_gu_init flags the deficits
-                hipLaunchKernelGGL(k_bf_round<false>, dim3(sgrid), dim3(BLK), 0, st, g, bseq, 0);
+                if (cpv) k_bf_round<false, true><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
+                else k_bf_round<false, false><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
                 ++bseq;
                 ++bf_launches;
             }
@@ -4242,15 +4369,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if (use_aug) {   // tail: walkers, hub distribution, walkers from what it fed
-                hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
-                if (nhit) hipLaunchKernelGGL(k_aug_hub, dim3(nhit), dim3(BLK), 0, st, g, sseq, walk_sl);
-                hipLaunchKernelGGL(k_augment, dim3(AUG_K2), dim3(WAVE), 0, st, g, sseq, 1, walk_sl);
+                KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, walk_sl);
+                if (nhit) KS_HOT(cpv, k_aug_hub, nhit, BLK, st, g, sseq, walk_sl);
+                KS_HOT(cpv, k_augment, AUG_K2, WAVE, st, g, sseq, 1, walk_sl);
                 // further passes retry the units left short at the listed nodes
                 for (int wp = 1; wp < walk_passes; ++wp)
-                    hipLaunchKernelGGL(k_augment, dim3(g.aug_k), dim3(WAVE), 0, st, g, sseq, 0, walk_sl);
+                    KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, walk_sl);
             }
             if ((e = hipEventRecord(s.cev[par][2], st)) != hipSuccess) return e;
-            for (int k = 0; k < gi; ++k) hipLaunchKernelGGL(k_sweep, dim3(wgrid), dim3(BLK), 0, st, g, k, sseq + k);
+            for (int k = 0; k < gi; ++k) KS_HOT(cpv, k_sweep, wgrid, BLK, st, g, k, sseq + k);
             if ((e = hipEventRecord(s.cev[par][3], st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 0);
             sseq += gi;
@@ -4623,6 +4750,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int vgrid = grid_for(hi, 2048);
     long long tot_cost = 0, tot_flow = 0;
     auto verify = [&](int* bad) -> int {
+        if (cp_dirty) {   // the compact solve's residuals back into the 32-B records first
+            hipLaunchKernelGGL(k_unpack_pos, dim3(grid_for(m2, 4096)), dim3(BLK), 0, st, (long long)m2,
+                               (const CPos*)s.cpos.p, s.pos.p);
+            cp_dirty = false;
+        }
         KS_CHECK(hipMemsetAsync(&s.ctl.p->verify_bad, 0, sizeof(int), st));
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
@@ -4700,6 +4832,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             if (pr < 0) return pr;
             if (cycle_log) std::fprintf(stderr, "canonical prices: %s after %d rounds\n", pr ? "set" : "not converged", used);
         }
+    }
+    if (cp_dirty) {   // (a solve that ended without verification: Pos stays the authoritative copy)
+        hipLaunchKernelGGL(k_unpack_pos, dim3(grid_for(m2, 4096)), dim3(BLK), 0, st, (long long)m2,
+                           (const CPos*)s.cpos.p, s.pos.p);
+        cp_dirty = false;
     }
     KS_CHECK(hipEventRecord(s.ev[7], st));
     unsigned long long hc[CTR_SHARDS * NCTR];

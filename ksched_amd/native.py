@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "ks_batch_load", "ks_batch_solve", "ks_batch_gather",
     "ks_batch_slots", "ks_batch_owner", "ks_batch_block_len", "ks_batch_unpack",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
 
@@ -54,7 +54,7 @@ class KsOpts(C.Structure):
                 ("bf_bound", C.c_int32), ("fwd_nodes", C.c_int32), ("cell_nodes", C.c_int32),
                 ("warm_shift", C.c_int32),
                 ("warm_canon", C.c_int32),
-                ("reserved", C.c_int32 * 1)]
+                ("compact_pos", C.c_int32)]
 
 
 class KsResult(C.Structure):
@@ -67,12 +67,12 @@ class KsResult(C.Structure):
                 ("gu_launches", C.c_uint64), ("ms_gu_kernels", C.c_double), ("warm_started", C.c_int32),
                 ("rebuilt", C.c_int32), ("recoveries", C.c_int32), ("solver", C.c_int32),
                 ("fs_launches", C.c_uint64), ("ms_fs_kernels", C.c_double), ("fwd_updates", C.c_uint64),
-                ("cells", C.c_int32), ("_pad3", C.c_int32), ("ms_cell_kernel", C.c_double),
+                ("cells", C.c_int32), ("compact", C.c_int32), ("ms_cell_kernel", C.c_double),
                 ("cell_ticks_max", C.c_uint64), ("cell_ticks_sum", C.c_uint64), ("fs_arc_scans", C.c_uint64),
                 ("cell_fallbacks", C.c_uint64), ("reserved2", C.c_uint64 * 2)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "_pad3", "reserved2")}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "reserved2")}
         names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d

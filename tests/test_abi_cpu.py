@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_default_opts():
     lib = native.load()
-    assert lib.ks_abi_version() == native.ABI_VERSION == 3
+    assert lib.ks_abi_version() == native.ABI_VERSION == 4
     o = native.default_opts()
     assert (o.alpha, o.verify, o.auto_sink) == (8, 1, 1)
     assert o.price_refine == 1 and o.gu_interval > 0 and o.warm_start == 0
@@ -63,7 +63,7 @@ int main(void) {
   P(ks_delta, cost); P(ks_delta, old_cost); P(ks_delta, excess);
   P(ks_result, status); P(ks_result, sweeps); P(ks_result, ms_phase); P(ks_result, n_nodes);
   P(ks_result, ms_gu_kernels); P(ks_result, rebuilt); P(ks_result, recoveries); P(ks_result, cell_fallbacks);
-  P(ks_opts, warm_start); P(ks_opts, walk_slack); P(ks_opts, fault_inject); P(ks_opts, walk_passes); P(ks_opts, tail_nodes); P(ks_opts, bf_bound); P(ks_opts, fwd_nodes); P(ks_opts, cell_nodes); P(ks_opts, warm_shift); P(ks_opts, warm_canon); P(ks_opts, reserved);
+  P(ks_opts, warm_start); P(ks_opts, walk_slack); P(ks_opts, fault_inject); P(ks_opts, walk_passes); P(ks_opts, tail_nodes); P(ks_opts, bf_bound); P(ks_opts, fwd_nodes); P(ks_opts, cell_nodes); P(ks_opts, warm_shift); P(ks_opts, warm_canon); P(ks_opts, compact_pos);
   P(ks_store_stats, superseded); P(ks_store_stats, residual_slots);
   P(ks_flow, flow);
   return 0;
@@ -97,7 +97,7 @@ def test_struct_layouts_match_bindings(tmp_path):
     for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels", "rebuilt", "recoveries", "cell_fallbacks"):
         assert getattr(native.KsResult, f).offset == out[f"ks_result.{f}"], f
     for f in ("warm_start", "walk_slack", "fault_inject", "walk_passes", "tail_nodes", "bf_bound", "fwd_nodes",
-              "cell_nodes", "warm_shift", "warm_canon", "reserved"):
+              "cell_nodes", "warm_shift", "warm_canon", "compact_pos"):
         assert getattr(native.KsOpts, f).offset == out[f"ks_opts.{f}"], f
 
 
