@@ -21,8 +21,16 @@ def main():
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 name = r["Kernel_Name"]
-                m = re.search(r"(k_\w+(<\w+>)?)\(", name)
-                short = m.group(1) if m else name.replace("(anonymous namespace)", "")[:40]
+                m = re.search(r"(k_\w+)(<([\w, ]+)>)?\(", name)
+                if m:   # the record-layout parameter (true/false last) is dropped: k_bf_round<false, true> → k_bf_round<false>
+                    targs = [t.strip() for t in (m.group(3) or "").split(",") if t.strip()]
+                    if m.group(1) in ("k_bf_round",) and len(targs) == 2:
+                        targs = targs[:1]
+                    elif m.group(1) in ("k_sweep", "k_saturate", "k_augment", "k_aug_hub", "k_fs_round", "k_fs_trace"):
+                        targs = []
+                    short = m.group(1) + (f"<{', '.join(targs)}>" if targs else "")
+                else:
+                    short = name.replace("(anonymous namespace)", "")[:40]
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short))
     rows.sort()
     st = np.array([r[0] for r in rows], np.int64)
