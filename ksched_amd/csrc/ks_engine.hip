@@ -2053,38 +2053,58 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
     }
     long long du = atom_load(&g.dist[ni(u)]);
     long long pu = g.p0[ni(u)];
+    int b0, en;
+    seg_of(g.p0, u, b0, en);
+    // A hop is two dependent levels: [u's records] → [their heads' records: price,
+    // distance, segment]; then the claim on the chosen arc, the next node's excess and
+    // the next node's first 64 records are all in flight at once (the head's segment
+    // came with its record), so the next hop starts from loaded records.
+    Pos q0{};
+    if (lane < en - b0) q0 = PL<CP>::ld(g, b0 + lane);
     int hops = 0, reached = 0, dummy = 0;
     for (int step = 0; step < AUG_STEPS; ++step) {
-        int b0, en;
-        seg_of(g.p0, u, b0, en);
         // the qualifying residual arc of least d(w) (ties: lowest position)
-        long long bd = INF64;
-        int ba = -1;
+        long long bd = INF64, bp = 0, br = 0;
+        unsigned long long bseg = 0;
+        int ba = -1, bw = 0, brev = 0;
         for (int base = b0; base < en; base += WAVE) {
             const int a = base + lane;
-            long long key = INF64;
+            Pos q{};
+            if (base == b0) q = q0;
+            else if (a < en) q = PL<CP>::ld(g, a);
+            long long key = INF64, pw = 0;
+            unsigned long long sg = 0;
             if (a < en) {
-                const Pos q = PL<CP>::ld_nr(g, a);
-                const long long r = PL<CP>::rc_atomic(g, a);   // other walkers claim with atomics
-                const long long cr = q.cost + pu - g.p0[ni(q.head)];
+                // (the record's residual may be stale under other walkers' claims: the CAS below corrects it)
+                pw = g.p0[ni(q.head)];
                 const long long dw = atom_load(&g.dist[ni(q.head)]);
-                if (r > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
+                sg = (unsigned long long)g.p0[ni(q.head) + ND_SEG];
+                const long long cr = q.cost + pu - pw;
+                if (q.rcap > 0 && cr <= slack * eps && (dw < du || (dw == du && cr < 0))) key = dw;
             }
             const long long mn = wave_min(key);
             if (mn < bd) {
                 const unsigned long long hit = __ballot(key == mn);
+                const int src = __ffsll((long long)hit) - 1;
                 bd = mn;
-                ba = base + __ffsll((long long)hit) - 1;
+                ba = base + src;
+                bw = __shfl(q.head, src);
+                brev = __shfl(q.rev, src);
+                br = __shfl(q.rcap, src);
+                bp = __shfl(pw, src);
+                bseg = (unsigned long long)__shfl((long long)sg, src);
             }
         }
         if (ba < 0) break;
-        // claim min(carry, residual) on arc ba
-        long long take = 0;
-        int w = 0;
+        // in flight together: the next node's first records, its excess, the claim
+        const int nb0 = (int)(unsigned)(bseg & 0xffffffffULL), nen = (int)(unsigned)(bseg >> 32);
+        Pos qn{};
+        if (lane < nen - nb0) qn = PL<CP>::ld(g, nb0 + lane);
+        long long take = 0, ew = 0;
         if (lane == 0) {
-            w = PL<CP>::head(g, ba);
-            long long r = PL<CP>::rc_atomic(g, ba);
-            for (;;) {
+            ew = atom_load(&g.excess[bw]);
+            long long r = br;
+            for (;;) {   // claim min(carry, residual) on arc ba
                 take = r < carry ? r : carry;
                 if (take <= 0) {
                     take = 0;
@@ -2094,34 +2114,33 @@ __global__ __launch_bounds__(WAVE) void k_augment(DG g, int sseq, int mode, int 
                 if (PL<CP>::cas_rc(g, ba, exp, r - take)) break;
                 r = exp;
             }
-            if (take > 0) PL<CP>::add_rc(g, PL<CP>::rev(g, ba), take);
+            if (take > 0) PL<CP>::add_rc(g, brev, take);
             if (take < carry) {   // the rest stays at u
                 atom_add(&g.excess[u], carry - take);
                 mark(g, F, u, dummy);
             }
         }
         take = __shfl(take, 0);
-        w = __shfl(w, 0);
         if (take == 0) {
             carry = 0;   // deposited at u above
             break;
         }
         carry = take;
         ++hops;
-        u = w;
+        u = bw;
         du = bd;
-        if (lane == 0) {
-            const long long e = atom_load(&g.excess[u]);
-            if (e < 0 || u >= g.hub_base) {   // a deficit (or a hub: the hub distribution takes over)
-                const long long now = atom_add_ret(&g.excess[u], carry) + carry;
-                if (now > 0) mark(g, F, u, dummy);
-                reached = e < 0 ? 1 : 0;
-                carry = 0;
-            }
+        if (lane == 0 && (ew < 0 || u >= g.hub_base)) {   // a deficit (or a hub: the hub distribution takes over)
+            const long long now = atom_add_ret(&g.excess[u], carry) + carry;
+            if (now > 0) mark(g, F, u, dummy);
+            reached = ew < 0 ? 1 : 0;
+            carry = 0;
         }
         carry = __shfl(carry, 0);
         if (carry == 0) break;
-        pu = g.p0[ni(u)];
+        pu = bp;
+        b0 = nb0;
+        en = nen;
+        q0 = qn;
     }
     if (lane == 0) {
         if (carry > 0) {   // hop limit or no qualifying arc: the units stay at u
@@ -4710,9 +4729,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // violate its ε (the previous optimum's arcs in [−1, 0) stay as they are)
         // per-cell fallback: the cold ε ladder, every phase saturating only the arcs
         // that violate its ε (the converged cells' optimal flows stay untouched)
-        const long long sat_thr = phases == 1 && use_warm && !fb
-                                      ? warm_thr
-                                      : ((pr_failed || fb || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
+        long long sat_thr = phases == 1 && use_warm && !fb
+                                ? warm_thr
+                                : ((pr_failed || fb || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
+#ifdef KS_EXP_SATV
+        {   // EXPERIMENT: phases after the first saturate only the arcs violating their ε
+            const bool lastp = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
+            if (phases > 1 && (KS_EXP_SATV == 2 || lastp)) sat_thr = eps;
+        }
+#endif
         pr_failed = false;
         const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
         // walk slack > 1 only while a finer phase or price refinement still follows

@@ -6,11 +6,13 @@ TAG=$1; WL=$2; REPS=${3:-3}; A=$4; B=$5
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-optargs() { local o=$1; local r=""; IFS=',' read -ra kv <<< "$o"; for x in "${kv[@]}"; do [ -n "$x" ] && r="$r --opt $x"; done; echo "$r"; }
+# an option spec may name a library variant: VARIANT=tag (libksmcmf_tag.so, _build.build_variant)
+optargs() { local o=$1; local r=""; IFS=',' read -ra kv <<< "$o"; for x in "${kv[@]}"; do case $x in VARIANT=*) ;; "") ;; *) r="$r --opt $x";; esac; done; echo "$r"; }
+variant() { local o=$1; IFS=',' read -ra kv <<< "$o"; for x in "${kv[@]}"; do case $x in VARIANT=*) echo "${x#VARIANT=}";; esac; done; }
 for i in $(seq 1 $REPS); do
     for v in A B; do
         if [ $v = A ]; then o=$A; else o=$B; fi
-        timeout -k 10 300 python -u bench.py $WL --cpu-baseline off $(optargs "$o") > "$OUT/${v}_$i.json" 2> "$OUT/${v}_$i.err" \
+        KS_LIB_VARIANT=$(variant "$o") timeout -k 10 300 python -u bench.py $WL --cpu-baseline off $(optargs "$o") > "$OUT/${v}_$i.json" 2> "$OUT/${v}_$i.err" \
             || { echo "bench $v $i failed"; tail -20 "$OUT/${v}_$i.err"; exit 1; }
         python - "$OUT/${v}_$i.json" "$v[$o]" <<'PY'
 import json, sys
