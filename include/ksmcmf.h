@@ -94,7 +94,11 @@ typedef struct ks_opts {
     int32_t  alpha;            /* cost-scaling factor per ε-phase (default 8)           */
     int32_t  verify;           /* run the on-device verifier after every solve (1)      */
     int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */
-    int32_t  price_refine;     /* certify optimality early by price refinement (1)      */
+    int32_t  price_refine;     /* certify optimality early [1]: 1 — the phase before the
+                                  final one drains, then price refinement cancels the
+                                  negative cycles it meets until it certifies the flow
+                                  (the final phase runs only if it gives up); 2 — the
+                                  final phase, then plain price refinement; 0 — off    */
     int32_t  gu_interval;      /* sweeps between global price updates (default 24)      */
     int32_t  warm_start;       /* 1: re-solve from the previous flow and prices after
                                   ks_apply_deltas (the first phase saturates only the
@@ -247,7 +251,9 @@ typedef struct ks_result {
                                   solver (step cap or wall-clock limit) and were re-solved
                                   on the multi-kernel engine, the other cells' optima
                                   kept (the status stays KS_OK)                         */
-    uint64_t reserved2[2];
+    uint64_t cycles_cancelled; /* negative cycles the cycle-cancelling finish cancelled
+                                  (ks_opts.price_refine 1)                  */
+    uint64_t reserved2[1];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

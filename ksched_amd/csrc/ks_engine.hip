@@ -115,6 +115,8 @@ struct Ctl {
     int bf_done;           // Bellman-Ford frontier drained (update converged)
     int verify_bad;
     int cp_bad;            // k_pack_pos: a value the 16-B record cannot hold (the solve reads Pos)
+    int cyc_n;             // cycle-cancelling refinement: cycles listed by the last search
+    int cyc_done;          //   and cancelled (whole refinement)
     int bf_count;          // Bellman-Ford rounds that did work (whole solve)
     int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
     int apply_act;         // the global-update apply seeded a non-empty frontier
@@ -1383,7 +1385,27 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
 // reverses of its CSR arcs a = (v→u): residual ucap(a) − rcap(a), cost −cost(a).
 // No returning atomics: a plain pre-check filters (a stale distance is only
 // larger), atomicMin commits, the flag store marks u for the next round.
-template <bool PR>
+//
+// PR = 2: price refinement that also finds negative cycles (the
+// cycle-cancelling finish). A node's dist slot then packs its distance (biased;
+// d ≤ 0 from d ≡ 0) above the node its parent arc leads to, so one 64-bit
+// atomicMin keeps each distance and its parent consistent, and the parent graph
+// holds the negative cycles that keep the refinement from converging.
+constexpr int PK_NB = 24;                              // node ids below 2^24
+constexpr long long PK_NONE = (1LL << PK_NB) - 1;      // no parent (d = 0 from the start)
+constexpr long long PK_BIAS = 1LL << 37;
+__device__ __forceinline__ long long pk(long long d, long long v) {
+    d = d < 1 - PK_BIAS ? 1 - PK_BIAS : (d > PK_BIAS - 1 ? PK_BIAS - 1 : d);
+    return ((d + PK_BIAS) << PK_NB) | v;
+}
+__device__ __forceinline__ long long pk_d(long long key) { return (key >> PK_NB) - PK_BIAS; }
+template <int PR>
+__device__ __forceinline__ long long dkey(long long raw) { return PR == 2 ? pk_d(raw) : raw; }
+// a < b as distances (packed keys: an equal distance through another parent is no improvement)
+template <int PR>
+__device__ __forceinline__ bool dless(long long a, long long b) { return PR == 2 ? (a >> PK_NB) < (b >> PK_NB) : a < b; }
+
+template <int PR>
 __device__ __forceinline__ long long arc_len(long long pu, long long ca, long long pv, long long eps) {
     long long len = floordiv(pu - ca - pv, eps) + 1;
     if (!PR) len = len < 0 ? 0 : (len > LEN_CAP ? LEN_CAP : len);
@@ -1392,7 +1414,7 @@ __device__ __forceinline__ long long arc_len(long long pu, long long ca, long lo
 
 // Offer distance cand to node u. Returns true when u is a grouped node whose
 // distance this call lowered (the caller then owns propagating it).
-template <bool PR>
+template <int PR>
 __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long long cand, long long du,
                                       long long B, long long* hub_min, int& out) {
     if (cand >= B) return false;   // at or beyond every listed excess node's distance (bounded update)
@@ -1400,20 +1422,20 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
         const int h = u - g.hub_base;
         if (h < HUB_LDS) {
             __hip_atomic_fetch_min(&hub_min[h], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (cand < atom_min_ret(&g.dist[ni(u)], cand)) {
+        } else if (dless<PR>(cand, atom_min_ret(&g.dist[ni(u)], cand))) {
             nf.hub[h] = 1;
             out = 1;
         }
         return false;
     }
-    if (cand >= du) return false;
+    if (!dless<PR>(cand, du)) return false;
     atom_min(&g.dist[ni(u)], cand);
     return true;
 }
 
 // Relax the in-arcs of a low-degree node u (≤ 8 arcs: tasks, PUs) right after
 // its distance dropped to du: a second hop inside the same round.
-template <bool PR, bool CP>
+template <int PR, bool CP>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
                                             int b0, int b1, long long eps, long long B, long long* hub_min, int& out) {
     // the records of all (≤ 8) arcs issued together; usually one in-arc carries
@@ -1436,7 +1458,8 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         const Pos q = PL<CP>::ld_nr(g, b);
         if (q.ucap - q.rcap > 0) {
             const int u2 = q.head;
-            const long long cand = du + arc_len<PR>(g.p0[ni(u2)], q.cost, pu, eps);
+            long long cand = du + arc_len<PR>(g.p0[ni(u2)], q.cost, pu, eps);
+            if (PR == 2) cand = pk(cand, u);
             if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, B, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
@@ -1456,7 +1479,8 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
             }
         const long long pu2 = g.p0[ni(u2)];
         const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
-        const long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
+        long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
+        if (PR == 2) cand = pk(cand, u);
         if (offer<PR>(g, nf, u2, cand, du2, B, hub_min, out)) {
             nf.flag[u2] = 1;
             out = 1;
@@ -1466,8 +1490,8 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
 
 // Relax in-arc (u→v) = reverse of CSR arc a = (v→u); residual ucap − rcap,
 // cost −cost(a). Loads are issued before the residual test (short chain).
-template <bool PR, bool CP>
-__device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, long long dv, long long pv,
+template <int PR, bool CP>
+__device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int v, int a, long long dv, long long pv,
                                          long long eps, long long B, long long* hub_min, int& out) {
     const Pos q = PL<CP>::ld_nr(g, a);
     const long long rin = q.ucap - q.rcap;
@@ -1482,8 +1506,8 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     int b0 = 0, b1 = 0;
     if (leaf) seg_of(g.p0, u, b0, b1);   // same record line as pu, du
     if (rin <= 0) return;
-    const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);
-    if (!offer<PR>(g, nf, u, cand, du, B, hub_min, out)) return;
+    const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);   // (dv decoded: a distance in every mode)
+    if (!offer<PR>(g, nf, u, PR == 2 ? pk(cand, v) : cand, du, B, hub_min, out)) return;
     if (leaf) {
         expand_leaf<PR, CP>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
     } else {
@@ -1492,7 +1516,7 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int a, lo
     }
 }
 
-template <int G, bool PR, bool CP>
+template <int G, int PR, bool CP>
 __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v, long long dv, long long pv, int b0,
                                              int en, long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
@@ -1502,14 +1526,14 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR, CP>(g, nf, a, dv, pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
             scans++;
         }
     }
 }
 
 // Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
-template <int C, bool PR, bool CP>
+template <int C, int PR, bool CP>
 __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, const WinFlag& f,
                                        long long eps, long long B, long long* hub_min, int& out, long long& scans) {
     constexpr int G = class_lanes(C);
@@ -1531,19 +1555,19 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
 }
 
 // One 64-arc chunk of a chunked-class node (its flag already tested).
-template <bool PR, bool CP>
+template <int PR, bool CP>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
                                          long long B, long long* hub_min, int& out, long long& scans) {
     const long long dv = atom_load(&g.dist[ni(ci.node)]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
-        relax_in<PR, CP>(g, N, a, dv, g.p0[ni(ci.node)], eps, B, hub_min, out);
+        relax_in<PR, CP>(g, N, ci.node, a, dkey<PR>(dv), g.p0[ni(ci.node)], eps, B, hub_min, out);
         scans++;
     }
 }
 
-template <int G, bool PR, bool CP>
+template <int G, int PR, bool CP>
 __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long B, long long* hub_min,
                                          int& out, long long& scans) {
     const int lig = lane_id() & (G - 1);
@@ -1560,7 +1584,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR, CP>(g, nf, a, dv, pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
             scans++;
         }
     }
@@ -1569,7 +1593,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
 // One Bellman-Ford round. dense = 1: every node (first round of an update).
 // dense_arg < 0: the round is dense iff it is the running update's first
 // (bf_seq0, set by the init kernel); ≥ 0: as given.
-template <bool PR, bool CP>
+template <int PR, bool CP>
 __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) {
     const int dense = dense_arg >= 0 ? dense_arg : (seq == g.ctl->bf_seq0 ? 1 : 0);
     __shared__ long long hub_min[HUB_LDS];
@@ -1612,7 +1636,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR, CP>(g, N, a, dv, pv, eps, B, hub_min, out);
+                        relax_in<PR, CP>(g, N, it.node, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
                         scans++;
                     }
                 }
@@ -1678,7 +1702,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         const long long val = hub_min[threadIdx.x];
         if (val < INF64) {
             long long* dx = &g.dist[ni(g.hub_base + threadIdx.x)];
-            if (val < atom_load(dx) && val < atom_min_ret(dx, val)) {
+            if (dless<PR>(val, atom_load(dx)) && dless<PR>(val, atom_min_ret(dx, val))) {
                 N.hub[threadIdx.x] = 1;
                 out = 1;
             }
@@ -1785,7 +1809,8 @@ __global__ void k_gu_init(DG g, int seq0, int list) {
         }
 }
 
-// PR init: dist = 0 everywhere, or dist = p (canonical prices: see k_pr_apply).
+// PR init: dist = 0 everywhere, or dist = p (canonical prices: see k_pr_apply);
+// from_p = 2: d = 0 with no parent, packed (the cycle-cancelling refinement).
 __global__ void k_pr_init(DG g, int seq0, int from_p) {
     clear_fronts(g, g.bf);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1794,7 +1819,7 @@ __global__ void k_pr_init(DG g, int seq0, int from_p) {
         for (int k = 0; k < 3; ++k) g.ctl->bfa[k] = 0;
     }
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK)
-        g.dist[ni(v)] = from_p ? g.p0[ni(v)] : 0;
+        g.dist[ni(v)] = from_p == 2 ? ((PK_BIAS << PK_NB) | PK_NONE) : from_p ? g.p0[ni(v)] : 0;
 }
 
 // End of a cycle: an update that has not converged is continued by the next
@@ -2492,13 +2517,140 @@ __global__ void k_perturb_price(DG g, int x, long long delta) {
 // over residual paths of length cost + 1 per arc, so p − d = −min(0, min_w dist(u, w)):
 // the canonical prices of the flow, the same for any prices it started from
 // (warm_canon: the drift of carried prices).
-__global__ void k_pr_apply(DG g) {
+__global__ void k_pr_apply(DG g, int packed) {
     if (!g.ctl->bf_done) return;
     const long long eps = g.ctl->eps;
     for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < g.n; v += (long long)gridDim.x * BLK) {
-        const long long np = g.p0[ni(v)] - eps * atom_load(&g.dist[ni(v)]);
+        const long long d = atom_load(&g.dist[ni(v)]);
+        const long long np = g.p0[ni(v)] - eps * (packed ? pk_d(d) : d);
         g.p0[ni(v)] = np;
         g.p1[ni(v)] = np;
+    }
+}
+
+// ------------------------------------------- cycle-cancelling refinement ---
+// The finish that replaces the final cost-scaling phase: the flow of
+// the last coarse phase is feasible and nearly optimal, and what keeps it from
+// optimality is a few negative cycles (CPU prototype tools/proto/cycle_cancel.c:
+// 11–13 on config 3, 24–120 arcs of cost −1…−4 each). The refinement's
+// Bellman-Ford (PR = 2) records each node's parent; when it has not converged
+// after a batch of rounds, the parent graph — one parent per node, so its cycles
+// are node-disjoint — is searched: pointer doubling (2^CYC_LOG steps) lands every
+// node of a cycle no longer than that, the least id of each window groups a
+// cycle, one thread per cycle walks it to check its cost (< 0) and bottleneck and
+// pushes the bottleneck around it, and the cycle's nodes rejoin the frontier.
+// The refinement then continues; once its frontier drains, every residual arc
+// meets d(u) ≤ d(v) + len(u, v): the prices p − d certify the flow optimal.
+constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
+constexpr int CYC_WALK = 1 << CYC_LOG;
+constexpr int kCycWaves = 512;   // cycles one search cancels at most
+
+// the parent of every node (itself for a root), its own id as the window minimum
+__global__ void k_cyc_par(DG g, int* __restrict__ J, int* __restrict__ M, int* __restrict__ onc) {
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
+        const long long v = atom_load(&g.dist[ni(u)]) & PK_NONE;
+        J[u] = v == PK_NONE ? (int)u : (int)v;
+        M[u] = (int)u;
+        onc[u] = 0;
+    }
+}
+// one doubling step: 2^k → 2^(k+1) steps ahead, and the least id over them
+__global__ void k_cyc_dbl(int n, const int* __restrict__ Ji, const int* __restrict__ Mi, int* __restrict__ Jo,
+                          int* __restrict__ Mo) {
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
+        const int j = Ji[u];
+        Jo[u] = Ji[j];
+        Mo[u] = min(Mi[u], Mi[j]);
+    }
+}
+// every node CYC_WALK steps ahead of some node lies on a cycle (the search's
+// depth is far below CYC_WALK); roots (their own parent) are skipped
+__global__ void k_cyc_mark(int n, const int* __restrict__ JK, const int* __restrict__ J0, int* __restrict__ onc) {
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
+        const int x = JK[u];
+        if (J0[x] != x) onc[x] = 1;
+    }
+}
+// list the marked nodes that are the least id of their window (one per cycle)
+__global__ void k_cyc_list(DG g, const int* __restrict__ onc, const int* __restrict__ MK, int* __restrict__ lst,
+                           int cap) {
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
+        if (!onc[u] || MK[u] != (int)u) continue;
+        const int i = atomicAdd(&g.ctl->cyc_n, 1);
+        if (i < cap) lst[i] = (int)u;
+    }
+}
+// The residual arc u → v of least cost (one wave scans u's segment).
+template <bool CP>
+__device__ __forceinline__ int cyc_arc(const DG& g, int u, int v, long long& cost, long long& cap) {
+    int b0, en;
+    seg_of(g.p0, u, b0, en);
+    long long best = INF64;
+    int ba = -1;
+    for (int base = b0; base < en; base += WAVE) {
+        const int a = base + lane_id();
+        long long key = INF64;
+        Pos q{};
+        if (a < en) {
+            q = PL<CP>::ld_nr(g, a);
+            if (q.head == v && q.rcap > 0) key = q.cost;
+        }
+        const long long mn = wave_min(key);
+        if (mn < best) {
+            best = mn;
+            const unsigned long long hit = __ballot(key == mn);
+            const int src = __ffsll((long long)hit) - 1;
+            ba = base + src;
+            cap = __shfl((long long)q.rcap, src);
+        }
+    }
+    cost = best;
+    return ba;
+}
+// One wave per listed cycle: walk it (checking that it closes within CYC_WALK
+// steps, that every parent arc is still residual, and that its cost is
+// negative), then push its bottleneck around it and put its nodes back into the
+// frontier the next refinement round reads (buffer seq).
+template <bool CP>
+__global__ __launch_bounds__(WAVE) void k_cyc_cancel(DG g, const int* __restrict__ J0, const int* __restrict__ lst,
+                                                    int cap, int seq) {
+    const int n = min(g.ctl->cyc_n, cap);
+    if ((int)blockIdx.x >= n) return;
+    const int s0 = lst[blockIdx.x];
+    long long sum = 0, delta = INF64;
+    int w = s0, len = 0;
+    bool ok = true;
+    do {
+        const int v = J0[w];
+        long long c = 0, r = 0;
+        if (cyc_arc<CP>(g, w, v, c, r) < 0) {
+            ok = false;
+            break;
+        }
+        sum += c;
+        delta = r < delta ? r : delta;
+        w = v;
+        ++len;
+    } while (w != s0 && len <= CYC_WALK);
+    if (!ok || w != s0 || sum >= 0 || delta <= 0 || delta >= INF64) return;
+    const Front F = g.bf[seq % 3];
+    w = s0;
+    do {
+        const int v = J0[w];
+        long long c = 0, r = 0;
+        const int a = cyc_arc<CP>(g, w, v, c, r);
+        if (lane_id() == 0) {
+            PL<CP>::set_rc(g, a, r - delta);
+            const Pos q = PL<CP>::ld(g, a);
+            PL<CP>::add_rc(g, q.rev, delta);
+            int dummy = 0;
+            mark(g, F, w, dummy);
+        }
+        w = v;
+    } while (w != s0);
+    if (lane_id() == 0) {
+        g.ctl->bfa[seq % 3] = 1;
+        atomicAdd(&g.ctl->cyc_done, 1);
     }
 }
 
@@ -2924,6 +3076,7 @@ struct EngineImpl {
     DBuf<Pos> pos;
     DBuf<CPos> cpos;               // the compact solve's 16-B positions (k_pack_pos)
     DBuf<int> crev;
+    DBuf<int> cyc;                 // cycle-cancelling refinement: parents, doubling buffers, marks, list
     DBuf<long long> excess;
     DBuf<long long> nd;            // node records [p0, dist, p1, pad] × nn
     DBuf<unsigned> keys_in, keys_out;
@@ -3019,7 +3172,7 @@ struct EngineImpl {
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
         first.release(); pos.release(); ent.release(); used.release(); scur.release(); perm.release(); iperm.release();
-        excess.release(); nd.release(); cpos.release(); crev.release();
+        excess.release(); nd.release(); cpos.release(); crev.release(); cyc.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
@@ -4092,6 +4245,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.rebuilt = s.csr_valid ? 0 : 1;
     res.recoveries = 0;
     res.cell_fallbacks = 0;
+    res.cycles_cancelled = 0;
     KS_CHECK(hipEventRecord(s.ev[0], st));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
@@ -4232,6 +4386,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // enqueued costs a whole extra cycle)
     const int kb_margin = o.bf_margin > 0 ? o.bf_margin : 6, kb_min = 8;
     bool pr_failed = false;   // the last phase's refinement did not certify the flow
+    // the cycle-cancelling finish replaces the final cost-scaling phase (ks_opts.price_refine
+    // 1, the default; 2: the final phase and plain refinement, as before round 5)
+    const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && nn < (int)PK_NONE;
+    const int prc_cap = 4096;   // refinement rounds before the final phase takes over
+    bool prc_tried = false;
     const int gi_tail = o.tail_sweeps > 0 ? std::max(2, std::min(MAXB, (int)o.tail_sweeps)) & ~1 : 4;
     // A phase that another phase follows may end with a few excess nodes left:
     // refine's start (saturate every negative reduced cost) accepts any
@@ -4284,16 +4443,20 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         s.h_scr[0] = e;
         return hipMemcpyAsync(&s.ctl.p->eps, &s.h_scr[0], sizeof(long long), hipMemcpyHostToDevice, st);
     };
-    auto bf_rounds = [&](bool pr, int k, bool first_dense) {
+    // mode 0: global update; 1: price refinement; 2: refinement with parents (cycle cancelling)
+    auto bf_rounds = [&](int mode, int k, bool first_dense) {
         for (int r = 0; r < k; ++r) {
             const int dense = (first_dense && r == 0) ? 1 : 0;
             const int grid = dense ? dgrid : sgrid;
-            if (pr) {
-                if (cpv) k_bf_round<true, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
-                else k_bf_round<true, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+            if (mode == 2) {
+                if (cpv) k_bf_round<2, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                else k_bf_round<2, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+            } else if (mode) {
+                if (cpv) k_bf_round<1, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                else k_bf_round<1, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
             } else {
-                if (cpv) k_bf_round<false, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
-                else k_bf_round<false, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                if (cpv) k_bf_round<0, true><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
+                else k_bf_round<0, false><<<dim3(grid), dim3(BLK), 0, st>>>(g, bseq, dense);
             }
             ++bseq;
             ++bf_launches;
@@ -4308,7 +4471,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         for (int batch = 0; used < cap; ++batch) {
             const int k = std::min(64, cap - used);
             KS_CHECK(hipEventRecord(s.kev[0], st));
-            bf_rounds(true, k, batch == 0);
+            bf_rounds(1, k, batch == 0);
             KS_CHECK(hipEventRecord(s.kev[1], st));
             used += k;
             KS_CHECK(read_ctl());
@@ -4318,11 +4481,71 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 break;
             }
         }
-        if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g);
+        if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g, 0);
         KS_CHECK(hipEventRecord(s.ev[7], st));
         KS_CHECK(hipEventSynchronize(s.ev[7]));
         ms_pr += ev_ms(s.ev[6], s.ev[7]);
         *rounds_used = used;
+        return ok;
+    };
+
+    // The cycle-cancelling finish: refinement rounds that record parents
+    // (PR = 2), and after every batch that has not converged a search of the parent
+    // graph that cancels the negative cycles it holds. 1 = certified (prices set),
+    // 0 = gave up within cap rounds (the final cost-scaling phase follows), < 0 error.
+    int prc_cycles = 0, prc_searches = 0;
+    auto prc_refine = [&](int* rounds_used, int cap) -> int {
+        KS_CHECK(hipEventRecord(s.ev[6], st));
+        KS_CHECK(s.cyc.ensure((size_t)7 * nn));
+        int* J0 = s.cyc.p;
+        int* Ja = J0 + nn;
+        int* Jb = Ja + nn;
+        int* Ma = Jb + nn;
+        int* Mb = Ma + nn;
+        int* onc = Mb + nn;
+        int* lst = onc + nn;
+        KS_CHECK(set_eps(1));
+        KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, sizeof(int), st));
+        hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, 2);
+        int used = 0, ok = 0;
+        for (int batch = 0; used < cap; ++batch) {
+            const int k = std::min(batch == 0 ? 32 : 16, cap - used);
+            KS_CHECK(hipEventRecord(s.kev[0], st));
+            bf_rounds(2, k, batch == 0);
+            KS_CHECK(hipEventRecord(s.kev[1], st));
+            used += k;
+            KS_CHECK(read_ctl());
+            ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
+            if (s.h_ctl->bf_done) {
+                ok = 1;
+                break;
+            }
+            // the parent graph: pointer doubling over CYC_WALK steps, then one wave per cycle
+            ++prc_searches;
+            hipLaunchKernelGGL(k_cyc_par, dim3(ngrid), dim3(BLK), 0, st, g, J0, Ma, onc);
+            KS_CHECK(hipMemcpyAsync(Ja, J0, (size_t)nn * sizeof(int), hipMemcpyDeviceToDevice, st));
+            for (int d = 0; d < CYC_LOG; ++d) {
+                if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Jb, Mb, Ja, Ma);
+                else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Ja, Ma, Jb, Mb);
+            }
+            const int* JK = (CYC_LOG & 1) ? Jb : Ja;
+            const int* MK = (CYC_LOG & 1) ? Mb : Ma;
+            hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, JK, (const int*)J0, onc);
+            KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_n, 0, sizeof(int), st));
+            hipLaunchKernelGGL(k_cyc_list, dim3(ngrid), dim3(BLK), 0, st, g, (const int*)onc, MK, lst, nn);
+            KS_HOT(cpv, k_cyc_cancel, kCycWaves, WAVE, st, g, (const int*)J0, (const int*)lst, kCycWaves, bseq);
+            cp_dirty = cpv;
+        }
+        if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g, 1);
+        KS_CHECK(hipEventRecord(s.ev[7], st));
+        KS_CHECK(hipEventSynchronize(s.ev[7]));
+        ms_pr += ev_ms(s.ev[6], s.ev[7]);
+        KS_CHECK(read_ctl());
+        prc_cycles += s.h_ctl->cyc_done;
+        *rounds_used = used;
+        if (cycle_log)
+            std::fprintf(stderr, "cycle-cancelling refinement: %s after %d rounds, %d searches, %d cycles cancelled\n",
+                         ok ? "certified" : "gave up", used, prc_searches, s.h_ctl->cyc_done);
         return ok;
     };
 
@@ -4379,8 +4602,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipError_t e = hipEventRecord(s.cev[par][0], st);
             if (e != hipSuccess) return e;
             for (int r = 0; r < kb; ++r) {   // sparse from the first round: k_gu_init flags the deficits
-                if (cpv) k_bf_round<false, true><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
-                else k_bf_round<false, false><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
+                if (cpv) k_bf_round<0, true><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
+                else k_bf_round<0, false><<<dim3(sgrid), dim3(BLK), 0, st>>>(g, bseq, 0);
                 ++bseq;
                 ++bf_launches;
             }
@@ -4740,16 +4963,34 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
 #endif
         pr_failed = false;
         const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
+        // the phase before the final one drains completely when the cycle-cancelling
+        // finish replaces the final phase
+        const long long eps_next = std::max<long long>(1, eps / alpha);
+        const bool before_last = !last_phase && !prc_tried &&
+                                 (eps_next / alpha < 1 || eps_next <= 1 || (use_pr && eps_next * pr_div < mult));
+        const bool prc_now = use_prc && before_last;
         // walk slack > 1 only while a finer phase or price refinement still follows
         // (ε > 1): a phase at ε = 1 must end 1-optimal (fault_inject bit 0 breaks
         // exactly this, for the certificate-recovery test)
         const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
-        const int rc = run_phase(eps, sat_thr, !last_phase, walk_sl);
+        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl);
         if (rc == KS_E_INFEASIBLE) {
             status = rc;
             break;
         }
         if (rc) return rc;
+        if (prc_now) {   // the feasible flow of the last coarse phase: cancel its negative cycles
+            prc_tried = true;
+            int used = 0;
+            const int pr = prc_refine(&used, prc_cap);
+            if (pr < 0) return pr;
+            if (pr == 1) {
+                eps = 1;
+                break;
+            }
+            pr_failed = true;   // the final phase follows, saturating only its violations
+            continue;
+        }
         // certify optimality early: a flow that is 1-optimal (scaled) is optimal.
         // Tried once ε is below 1/32 of a cost unit, where it usually succeeds.
         if (use_pr && eps > 1 && eps * pr_div < mult) {
@@ -4913,6 +5154,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.cell_ticks_max = cticks_max;
     res.cell_ticks_sum = cticks_sum;
     res.status = status;
+    res.cycles_cancelled = (uint64_t)prc_cycles;
     KS_CHECK(hipMemsetAsync(s.n_cshift.p, 0, s.nstore * sizeof(unsigned long long), st));
     if (status == KS_OK) {
         KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));
