@@ -131,7 +131,11 @@ typedef struct ks_opts {
                                   its rows in ks_batch_gather (every rank must still
                                   reach the collective and return the error). Bit 3
                                   (ks_batch_create*): rank 0's receive buffer
-                                  allocation fails in ks_batch_gather (the same).     */
+                                  allocation fails in ks_batch_gather (the same).
+                                  Bit 4 (ks_batch_create*): the middle cell of the
+                                  batch gives up in the cell solver (re-solved on the
+                                  engine). Bit 5: the cycle-cancelling finish gives
+                                  up after its first batch (the final phase runs).    */
     int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
                                   cycle [1]; later passes retry units left short        */
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —

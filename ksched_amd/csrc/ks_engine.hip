@@ -4389,7 +4389,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // the cycle-cancelling finish replaces the final cost-scaling phase (ks_opts.price_refine
     // 1, the default; 2: the final phase and plain refinement, as before round 5)
     const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && nn < (int)PK_NONE;
-    const int prc_cap = 4096;   // refinement rounds before the final phase takes over
+    // refinement rounds before the final phase takes over (TESTS ONLY, fault_inject bit 5: one batch)
+    const int prc_cap = (o.fault_inject & 32) ? 32 : 4096;
     bool prc_tried = false;
     const int gi_tail = o.tail_sweeps > 0 ? std::max(2, std::min(MAXB, (int)o.tail_sweeps)) & ~1 : 4;
     // A phase that another phase follows may end with a few excess nodes left:

@@ -404,3 +404,30 @@ def test_cell_range_fallback_on_a_warm_start():
         assert (r1.cost, r1.flow) == want
         r2 = ctx.solve()
         assert (r2.cost, r2.flow) == want
+
+
+@pytest.mark.parametrize("opts", [{}, {"price_refine": 2}, {"fault_inject": 32}, {"compact_pos": -1}])
+def test_cycle_cancelling_finish(opts):
+    """The cycle-cancelling finish (ks_opts.price_refine 1): the last
+    coarse phase drains, then price refinement cancels the negative cycles of its
+    parent graph until it certifies the flow. Against the plain final phase
+    (price_refine 2), the finish giving up after one batch (fault_inject bit 5: the
+    final phase follows), and the 32-B records: the same optimum as the oracle on
+    config-2-sized cells (engine) and random graphs, every flow re-verified."""
+    cc = 0
+    with native.Context(0, cell_nodes=-1, **opts) as c2:
+        for seed in (2, 7, 11):
+            g = gen.quincy(10_000, 1_000, 25, 100, seed)
+            st, c, fv, _ = ko.cost_scaling(g)
+            assert st == 0
+            r = solve_and_check(c2, g, c, fv)
+            cc += r.raw["cycles_cancelled"]
+            assert r.raw["recoveries"] == 0
+        for trial, g in random_graphs(9191, 12):
+            st, c, fv, _, _ = ko.ssp(g)
+            if st == 0:
+                solve_and_check(c2, g, c, fv)
+    if opts.get("price_refine", 1) == 2:
+        assert cc == 0
+    elif not opts.get("fault_inject"):
+        assert cc > 0, "no negative cycle was cancelled on three config-2 cells"
