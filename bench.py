@@ -132,6 +132,7 @@ def roofline_of(results, workload: str):
             "note": "SURVEY 8(d): B_work / t_solve over all timed solves; b_pass = one read of the "
                     "residual graph, the floor any iterative solve sits above"}
     pf = pmc_file(workload)
+    k = {}
     if pf:
         pmc = json.load(open(pf))
         k = pmc.get("kernels", {}).get(kernel, {})
@@ -141,6 +142,24 @@ def roofline_of(results, workload: str):
                                   "calibrated_bytes_per_launch": k.get("calibrated_bytes_per_launch"),
                                   "atomics_per_launch": k.get("tcc_atomic_per_launch"),
                                   "note": pmc.get("note")}
+    if kernel == "k_cell":
+        # the cell solver's scans and relaxations are served by LDS and
+        # L2, so 24 B per unit is not HBM traffic. Its HBM line is the PMC counter bytes
+        # (FETCH_SIZE + WRITE_SIZE per launch) over this run's event-timed launch, and its
+        # compute line the VALU issue rate of the same profile (2 wave64 VALU per CU-cycle).
+        line["achieved_algorithmic_24B"] = line["achieved"]
+        line["bytes_per_unit"] = None
+        line["bytes_per_launch"] = None
+        raw = k.get("raw_bytes_per_launch")
+        t = ms / max(1, n) / 1e3
+        if raw and t > 0:
+            line["achieved"] = round(raw / t / 1e9, 3)
+            line["frac"] = round(raw / t / 1e9 / HBM_PEAK_GBS, 6)
+            line["bytes_source"] = "PMC counter bytes per launch (traffic_source)"
+        else:
+            line["achieved"], line["frac"] = None, None
+        if k.get("valu"):
+            line["valu"] = k["valu"]
     return line
 
 

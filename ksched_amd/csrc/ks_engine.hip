@@ -4770,7 +4770,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         KS_CHECK(read_ctl());
         const long long viol = s.h_ctl->gu_L;
-        long long e0 = std::max<long long>(1, std::min<long long>({viol, 8 * mult, eps}));
+#ifndef KS_EXP_WARM_UNITS
+#define KS_EXP_WARM_UNITS 8
+#endif
+        long long e0 = std::max<long long>(1, std::min<long long>({viol, KS_EXP_WARM_UNITS * mult, eps}));
         if (s.cell_layout && (alpha & (alpha - 1)) == 0)   // a power of two ≥ the violation (cell ladder)
             while (e0 & (e0 - 1)) e0 += e0 & -e0;
         warm_thr = e0;

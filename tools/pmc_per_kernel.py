@@ -14,8 +14,18 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(k_\w+(<\w+>)?)\(", name)
-    return m.group(1) if m else name.split("(")[0][-60:]
+    """k_bf_round<false, true>(…) → k_bf_round<false>; k_sweep<true>(…) → k_sweep: the
+    record-layout template argument (round 5, the last one) is dropped."""
+    m = re.search(r"(k_\w+)(<([\w, ]+)>)?\(", name)
+    if not m:
+        return name.split("(")[0][-60:]
+    targs = [t.strip() for t in (m.group(3) or "").split(",") if t.strip()]
+    if m.group(1) == "k_bf_round" and len(targs) == 2:
+        targs = targs[:1]
+    elif m.group(1) in ("k_sweep", "k_saturate", "k_augment", "k_aug_hub", "k_fs_round", "k_fs_trace",
+                        "k_cyc_cancel"):
+        targs = []
+    return m.group(1) + (f"<{', '.join(targs)}>" if targs else "")
 
 
 def main():

@@ -30,7 +30,7 @@ def per_kernel(dirs):
 
 def main():
     pmc, cal, date = sys.argv[1], sys.argv[2], sys.argv[3]
-    k = per_kernel([os.path.join(pmc, p) for p in ("fetch", "write", "atom", "ta")])
+    k = per_kernel([os.path.join(pmc, p) for p in ("fetch", "write", "atom", "ta", "valu") if os.path.isdir(os.path.join(pmc, p))])
     if cal.endswith(".json"):   # a committed profile's calibration (the calibration is a one-off)
         calib = json.load(open(cal))["calibration"]
     else:
@@ -87,6 +87,19 @@ def main():
                "tcc_atomic_per_launch": round(per["TCC_ATOMIC_sum"], 1),
                "ea_atomic_per_launch": round(per["TCC_EA0_ATOMIC_sum"], 1),
                "ta_flat_atomic_wavefronts_per_launch": round(per["TA_FLAT_ATOMIC_WAVEFRONTS_sum"], 1)}
+        src = k.get(name, {})
+        if src.get("SQ_INSTS_VALU") is not None and src.get("SQ_BUSY_CU_CYCLES"):
+            nv = max(1, int(src.get("SQ_INSTS_VALU_dispatches", 1)))
+            ipc = src["SQ_INSTS_VALU"] / src["SQ_BUSY_CU_CYCLES"]
+            rec["valu"] = {"insts_per_launch": round(src["SQ_INSTS_VALU"] / nv, 1),
+                           "busy_cu_cycles_per_launch": round(src["SQ_BUSY_CU_CYCLES"] / nv, 1),
+                           "valu_per_cu_cycle": round(ipc, 4),
+                           "peak_per_cu_cycle": 2.0,
+                           "frac": round(ipc / 2.0, 4),
+                           "note": "SQ_INSTS_VALU (wave64 VALU instructions) / SQ_BUSY_CU_CYCLES (cycles the CUs "
+                                   "running the kernel were busy, summed over CUs); a CDNA4 CU issues at most 2 "
+                                   "wave64 VALU per cycle (4 SIMD-32, a wave64 instruction over 2 cycles; "
+                                   "MI355X_MICROARCH.md)"}
         t = times.get(name)
         if t and t["total_us"] > 0:
             rec["device_us_total"] = round(t["total_us"], 1)
