@@ -24,8 +24,9 @@
 //             (≤ 512), a 16- or 32-lane group per node (≤ 32: machines), one
 //             thread per node (≤ 8: tasks, PUs — a bitmask of the positions that
 //             need a push / relaxation / saturation, then only those).
-//   VALU      a solve is VALU-bound on its CU (PMC: ~7.5e7 VALU instructions over
-//             ~1.1e8 cycles); batched record loads are issued unconditionally and
+//   latency   a solve issues 29 % of its CU's VALU ceiling (PMC: 7.5e7 wave64 VALU
+//             instructions over 1.3e8 cycles, against 2 per cycle): it is bound by its
+//             dependent chains and barriers; batched record loads are issued unconditionally and
 //             pinned (a load in a lane-conditional branch waits there), lane-group
 //             scans are DPP with the group's last lane as leader.
 //   snapshot  sweeps read one price array and defer relabels to the end of the
@@ -778,7 +779,7 @@ __device__ __forceinline__ void sat_leaf(const CellArgs& A, K& k, const int (&v)
 // relaxation, a saturation — and a ctz loop then takes only those, re-reading the
 // record (an L1 hit). A task has about one such position, so a wave runs the
 // expensive path about once per 64 tasks instead of once per position index
-// (the cell solve is VALU-bound on its CU: DESIGN §3.5).
+// (fewer VALU instructions per wave, and fewer lanes idle in the expensive path).
 template <int MAXP>
 __device__ __forceinline__ int thr_load(const CellArgs& A, const K& k, int v, int& b0, int4 (&qr)[MAXP]) {
     int en;
