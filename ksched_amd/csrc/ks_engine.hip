@@ -115,8 +115,7 @@ struct Ctl {
     int bf_done;           // Bellman-Ford frontier drained (update converged)
     int verify_bad;
     int cp_bad;            // k_pack_pos: a value the 16-B record cannot hold (the solve reads Pos)
-    int cyc_n;             // cycle-cancelling refinement: cycles listed by the last search
-    int cyc_done;          //   and cancelled (whole refinement)
+    int cyc_done;          // cycle-cancelling refinement: cycles cancelled
     int bf_count;          // Bellman-Ford rounds that did work (whole solve)
     int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
     int apply_act;         // the global-update apply seeded a non-empty frontier
@@ -1388,10 +1387,12 @@ __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
 //
 // PR = 2: price refinement that also finds negative cycles (the
 // cycle-cancelling finish). A node's dist slot then packs its distance (biased;
-// d ≤ 0 from d ≡ 0) above the node its parent arc leads to, so one 64-bit
-// atomicMin keeps each distance and its parent consistent, and the parent graph
-// holds the negative cycles that keep the refinement from converging.
-constexpr int PK_NB = 24;                              // node ids below 2^24
+// d ≤ 0 from d ≡ 0) above its parent arc — the position, in the parent's
+// segment, of the arc that ends at the node (the parent arc itself is its
+// reverse) — so one 64-bit atomicMin keeps each distance and its parent
+// consistent, and the parent graph holds the negative cycles that keep the
+// refinement from converging.
+constexpr int PK_NB = 24;                              // positions below 2^24
 constexpr long long PK_NONE = (1LL << PK_NB) - 1;      // no parent (d = 0 from the start)
 constexpr long long PK_BIAS = 1LL << 37;
 __device__ __forceinline__ long long pk(long long d, long long v) {
@@ -1459,7 +1460,7 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         if (q.ucap - q.rcap > 0) {
             const int u2 = q.head;
             long long cand = du + arc_len<PR>(g.p0[ni(u2)], q.cost, pu, eps);
-            if (PR == 2) cand = pk(cand, u);
+            if (PR == 2) cand = pk(cand, b);
             if (offer<PR>(g, nf, u2, cand, u2 < g.hub_base ? g.dist[ni(u2)] : INF64, B, hub_min, out)) {
                 nf.flag[u2] = 1;
                 out = 1;
@@ -1480,7 +1481,7 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
         const long long pu2 = g.p0[ni(u2)];
         const long long du2 = u2 < g.hub_base ? g.dist[ni(u2)] : INF64;
         long long cand = du + arc_len<PR>(pu2, c2, pu, eps);
-        if (PR == 2) cand = pk(cand, u);
+        if (PR == 2) cand = pk(cand, b0 + k);
         if (offer<PR>(g, nf, u2, cand, du2, B, hub_min, out)) {
             nf.flag[u2] = 1;
             out = 1;
@@ -1507,7 +1508,7 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int v, in
     if (leaf) seg_of(g.p0, u, b0, b1);   // same record line as pu, du
     if (rin <= 0) return;
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);   // (dv decoded: a distance in every mode)
-    if (!offer<PR>(g, nf, u, PR == 2 ? pk(cand, v) : cand, du, B, hub_min, out)) return;
+    if (!offer<PR>(g, nf, u, PR == 2 ? pk(cand, a) : cand, du, B, hub_min, out)) return;
     if (leaf) {
         expand_leaf<PR, CP>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
     } else {
@@ -2543,15 +2544,27 @@ __global__ void k_pr_apply(DG g, int packed) {
 // meets d(u) ≤ d(v) + len(u, v): the prices p − d certify the flow optimal.
 constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
 constexpr int CYC_WALK = 1 << CYC_LOG;
-constexpr int kCycWaves = 512;   // cycles one search cancels at most
+constexpr int kForceNodes = 64;   // the forced tail of the phase before the finish starts at this many excess nodes
 
-// the parent of every node (itself for a root), its own id as the window minimum
-__global__ void k_cyc_par(DG g, int* __restrict__ J, int* __restrict__ M, int* __restrict__ onc) {
+// The parent of every node (itself for a root) from its key's position a (the
+// parent v is the head of a's reverse); its own id as the window minimum; the
+// per-group sums reset.
+template <bool CP>
+__global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* __restrict__ M,
+                          int* __restrict__ onc, int* __restrict__ R, long long* __restrict__ gsum,
+                          long long* __restrict__ gcap, int* __restrict__ gbad) {
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
-        const long long v = atom_load(&g.dist[ni(u)]) & PK_NONE;
-        J[u] = v == PK_NONE ? (int)u : (int)v;
+        const long long a = atom_load(&g.dist[ni(u)]) & PK_NONE;
+        int v = (int)u;
+        if (a != PK_NONE) v = PL<CP>::head(g, PL<CP>::rev(g, (int)a));
+        J0[u] = v;
+        J[u] = v;
         M[u] = (int)u;
+        R[u] = (int)a;
         onc[u] = 0;
+        gsum[u] = 0;
+        gcap[u] = INF64;
+        gbad[u] = 0;
     }
 }
 // one doubling step: 2^k → 2^(k+1) steps ahead, and the least id over them
@@ -2563,95 +2576,60 @@ __global__ void k_cyc_dbl(int n, const int* __restrict__ Ji, const int* __restri
         Mo[u] = min(Mi[u], Mi[j]);
     }
 }
-// every node CYC_WALK steps ahead of some node lies on a cycle (the search's
-// depth is far below CYC_WALK); roots (their own parent) are skipped
+// every node CYC_WALK steps ahead of some node lies on a cycle (the refinement's
+// parent chains are far shorter than CYC_WALK); roots (their own parent) are skipped
 __global__ void k_cyc_mark(int n, const int* __restrict__ JK, const int* __restrict__ J0, int* __restrict__ onc) {
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
         const int x = JK[u];
         if (J0[x] != x) onc[x] = 1;
     }
 }
-// list the marked nodes that are the least id of their window (one per cycle)
-__global__ void k_cyc_list(DG g, const int* __restrict__ onc, const int* __restrict__ MK, int* __restrict__ lst,
-                           int cap) {
+// Each cycle node adds its parent arc (u → v, the reverse of position R[u]) to its
+// group — the least id of its window, the cycle's least id when the cycle has at
+// most CYC_WALK nodes: cost sum, bottleneck residual. A group whose nodes disagree
+// on the group (a longer cycle) or whose arc is not residual is marked bad.
+template <bool CP>
+__global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
+                            const int* __restrict__ R, long long* __restrict__ gsum, long long* __restrict__ gcap,
+                            int* __restrict__ gbad) {
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
-        if (!onc[u] || MK[u] != (int)u) continue;
-        const int i = atomicAdd(&g.ctl->cyc_n, 1);
-        if (i < cap) lst[i] = (int)u;
+        if (!onc[u] || J0[u] == (int)u) continue;
+        const int m = MK[u], mn = MK[J0[u]];
+        if (mn != m) {
+            gbad[m] = 1;
+            gbad[mn] = 1;
+        }
+        const Pos q = PL<CP>::ld_nr(g, R[u]);
+        const long long res = q.ucap - q.rcap;   // residual of the reverse: the arc u → v
+        if (res <= 0) gbad[m] = 1;
+        atom_add(&gsum[m], -q.cost);
+        __hip_atomic_fetch_min(&gcap[m], res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-// The residual arc u → v of least cost (one wave scans u's segment).
+// Cancel every good negative group: each of its nodes pushes the bottleneck along
+// its own parent arc (the arcs of different nodes are different positions), and
+// rejoins the frontier the next refinement round reads (buffer seq).
 template <bool CP>
-__device__ __forceinline__ int cyc_arc(const DG& g, int u, int v, long long& cost, long long& cap) {
-    int b0, en;
-    seg_of(g.p0, u, b0, en);
-    long long best = INF64;
-    int ba = -1;
-    for (int base = b0; base < en; base += WAVE) {
-        const int a = base + lane_id();
-        long long key = INF64;
-        Pos q{};
-        if (a < en) {
-            q = PL<CP>::ld_nr(g, a);
-            if (q.head == v && q.rcap > 0) key = q.cost;
-        }
-        const long long mn = wave_min(key);
-        if (mn < best) {
-            best = mn;
-            const unsigned long long hit = __ballot(key == mn);
-            const int src = __ffsll((long long)hit) - 1;
-            ba = base + src;
-            cap = __shfl((long long)q.rcap, src);
-        }
-    }
-    cost = best;
-    return ba;
-}
-// One wave per listed cycle: walk it (checking that it closes within CYC_WALK
-// steps, that every parent arc is still residual, and that its cost is
-// negative), then push its bottleneck around it and put its nodes back into the
-// frontier the next refinement round reads (buffer seq).
-template <bool CP>
-__global__ __launch_bounds__(WAVE) void k_cyc_cancel(DG g, const int* __restrict__ J0, const int* __restrict__ lst,
-                                                    int cap, int seq) {
-    const int n = min(g.ctl->cyc_n, cap);
-    if ((int)blockIdx.x >= n) return;
-    const int s0 = lst[blockIdx.x];
-    long long sum = 0, delta = INF64;
-    int w = s0, len = 0;
-    bool ok = true;
-    do {
-        const int v = J0[w];
-        long long c = 0, r = 0;
-        if (cyc_arc<CP>(g, w, v, c, r) < 0) {
-            ok = false;
-            break;
-        }
-        sum += c;
-        delta = r < delta ? r : delta;
-        w = v;
-        ++len;
-    } while (w != s0 && len <= CYC_WALK);
-    if (!ok || w != s0 || sum >= 0 || delta <= 0 || delta >= INF64) return;
+__global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
+                           const int* __restrict__ R, const long long* __restrict__ gsum,
+                           const long long* __restrict__ gcap, const int* __restrict__ gbad, int seq) {
     const Front F = g.bf[seq % 3];
-    w = s0;
-    do {
-        const int v = J0[w];
-        long long c = 0, r = 0;
-        const int a = cyc_arc<CP>(g, w, v, c, r);
-        if (lane_id() == 0) {
-            PL<CP>::set_rc(g, a, r - delta);
-            const Pos q = PL<CP>::ld(g, a);
-            PL<CP>::add_rc(g, q.rev, delta);
-            int dummy = 0;
-            mark(g, F, w, dummy);
-        }
-        w = v;
-    } while (w != s0);
-    if (lane_id() == 0) {
-        g.ctl->bfa[seq % 3] = 1;
-        atomicAdd(&g.ctl->cyc_done, 1);
+    int out = 0, cyc = 0;
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
+        if (!onc[u] || J0[u] == (int)u) continue;
+        const int m = MK[u];
+        const long long dl = gcap[m];
+        if (gbad[m] || gsum[m] >= 0 || dl <= 0 || dl >= INF64) continue;
+        const int a = R[u];
+        const Pos q = PL<CP>::ld(g, a);
+        PL<CP>::set_rc(g, a, q.rcap + dl);        // the arc u → v is rev(a): its residual falls by dl
+        PL<CP>::add_rc(g, q.rev, -dl);
+        mark(g, F, (int)u, out);
+        cyc += u == m;
     }
+    if (__any(out) && lane_id() == 0) g.ctl->bfa[seq % 3] = 1;
+    cyc = (int)wave_sum(cyc);
+    if (cyc && lane_id() == 0) atomicAdd(&g.ctl->cyc_done, cyc);
 }
 
 // ================================================================ verify ===
@@ -3076,7 +3054,8 @@ struct EngineImpl {
     DBuf<Pos> pos;
     DBuf<CPos> cpos;               // the compact solve's 16-B positions (k_pack_pos)
     DBuf<int> crev;
-    DBuf<int> cyc;                 // cycle-cancelling refinement: parents, doubling buffers, marks, list
+    DBuf<int> cyc;                 // cycle-cancelling refinement: parents, doubling buffers, marks, arcs
+    DBuf<long long> cyc64;         //   and per-group cost sums and bottlenecks
     DBuf<long long> excess;
     DBuf<long long> nd;            // node records [p0, dist, p1, pad] × nn
     DBuf<unsigned> keys_in, keys_out;
@@ -3172,7 +3151,7 @@ struct EngineImpl {
         a_cost.release(); a_alive.release(); hkey.release(); hval.release(); hlast.release(); sctl.release();
         d_recs.release(); d_edits.release(); rec_ent.release();
         first.release(); pos.release(); ent.release(); used.release(); scur.release(); perm.release(); iperm.release();
-        excess.release(); nd.release(); cpos.release(); crev.release(); cyc.release();
+        excess.release(); nd.release(); cpos.release(); crev.release(); cyc.release(); cyc64.release();
         keys_in.release(); keys_out.release(); vals_in.release(); vals_out.release(); pos_of.release(); deg.release();
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
@@ -4388,7 +4367,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     bool pr_failed = false;   // the last phase's refinement did not certify the flow
     // the cycle-cancelling finish replaces the final cost-scaling phase (ks_opts.price_refine
     // 1, the default; 2: the final phase and plain refinement, as before round 5)
-    const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && nn < (int)PK_NONE;
+    const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && s.m2cap < PK_NONE;
     // refinement rounds before the final phase takes over (TESTS ONLY, fault_inject bit 5: one batch)
     const int prc_cap = (o.fault_inject & 32) ? 32 : 4096;
     bool prc_tried = false;
@@ -4497,14 +4476,18 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     int prc_cycles = 0, prc_searches = 0;
     auto prc_refine = [&](int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
-        KS_CHECK(s.cyc.ensure((size_t)7 * nn));
+        KS_CHECK(s.cyc.ensure((size_t)8 * nn));
+        KS_CHECK(s.cyc64.ensure((size_t)2 * nn));
         int* J0 = s.cyc.p;
         int* Ja = J0 + nn;
         int* Jb = Ja + nn;
         int* Ma = Jb + nn;
         int* Mb = Ma + nn;
         int* onc = Mb + nn;
-        int* lst = onc + nn;
+        int* R = onc + nn;
+        int* gbad = R + nn;
+        long long* gsum = s.cyc64.p;
+        long long* gcap = gsum + nn;
         KS_CHECK(set_eps(1));
         KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, sizeof(int), st));
         hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, 2);
@@ -4521,10 +4504,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 ok = 1;
                 break;
             }
-            // the parent graph: pointer doubling over CYC_WALK steps, then one wave per cycle
+            // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
+            // their least id, every good negative one cancelled in parallel
             ++prc_searches;
-            hipLaunchKernelGGL(k_cyc_par, dim3(ngrid), dim3(BLK), 0, st, g, J0, Ma, onc);
-            KS_CHECK(hipMemcpyAsync(Ja, J0, (size_t)nn * sizeof(int), hipMemcpyDeviceToDevice, st));
+            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad);
             for (int d = 0; d < CYC_LOG; ++d) {
                 if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Jb, Mb, Ja, Ma);
                 else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Ja, Ma, Jb, Mb);
@@ -4532,9 +4515,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             const int* JK = (CYC_LOG & 1) ? Jb : Ja;
             const int* MK = (CYC_LOG & 1) ? Mb : Ma;
             hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, JK, (const int*)J0, onc);
-            KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_n, 0, sizeof(int), st));
-            hipLaunchKernelGGL(k_cyc_list, dim3(ngrid), dim3(BLK), 0, st, g, (const int*)onc, MK, lst, nn);
-            KS_HOT(cpv, k_cyc_cancel, kCycWaves, WAVE, st, g, (const int*)J0, (const int*)lst, kCycWaves, bseq);
+            KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
+                   gbad);
+            KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
+                   (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
             cp_dirty = cpv;
         }
         if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g, 1);
@@ -4557,7 +4541,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // nodes left for the next, finer one. walk_sl: the tail walks' slack (1 when the
     // phase must end ε-optimal at ε = 1). Returns KS_OK, KS_E_INFEASIBLE (status),
     // or a device / convergence error.
-    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl) -> int {
+    // force_tail: the phase the cycle-cancelling finish follows. Once ≤ kForceNodes
+    // nodes hold excess, its tail is routed by the walks alone with no reduced-cost
+    // limit (down the updates' distances, so along near-shortest paths): the flow
+    // becomes feasible in a few updates instead of the tail's dozens, and the few
+    // negative cycles this leaves are cancelled with the others.
+    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl,
+                         bool force_tail = false) -> int {
         KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
         KS_HOT(cpv, k_saturate, fgrid, BLK, st, g, sat_thr);
@@ -4570,6 +4560,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
         int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
+        bool force = false;   // the forced tail is running (force_tail)
+        int wsl = walk_sl;    // the walks' slack (unlimited while forced)
+        int force_stall = 0;
+        long long force_units = -1;
+        const int force_sl = (int)std::min<long long>(1LL << 30, (1LL << 61) / std::max<long long>(1, eps_ph));
         int rc = KS_OK;
         // Forward cycle: nupd × [init (or continue the pending search)][kf rounds][apply]
         // [trace][end], then the cycle end; no sweeps (the trace routes the units). An
@@ -4612,12 +4607,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             hipLaunchKernelGGL(k_gu_max, dim3(ngrid), dim3(BLK), 0, st, g);
             hipLaunchKernelGGL(k_gu_apply, dim3(ngrid), dim3(BLK), 0, st, g, sseq);
             if (use_aug) {   // tail: walkers, hub distribution, walkers from what it fed
-                KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, walk_sl);
-                if (nhit) KS_HOT(cpv, k_aug_hub, nhit, BLK, st, g, sseq, walk_sl);
-                KS_HOT(cpv, k_augment, AUG_K2, WAVE, st, g, sseq, 1, walk_sl);
+                KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, wsl);
+                if (nhit) KS_HOT(cpv, k_aug_hub, nhit, BLK, st, g, sseq, wsl);
+                KS_HOT(cpv, k_augment, AUG_K2, WAVE, st, g, sseq, 1, wsl);
                 // further passes retry the units left short at the listed nodes
                 for (int wp = 1; wp < walk_passes; ++wp)
-                    KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, walk_sl);
+                    KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, wsl);
             }
             if ((e = hipEventRecord(s.cev[par][2], st)) != hipSuccess) return e;
             for (int k = 0; k < gi; ++k) KS_HOT(cpv, k_sweep, wgrid, BLK, st, g, k, sseq + k);
@@ -4708,7 +4703,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             if (cycle_log) {
                 std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d units %lld n_exc %d walks %d/%d",
-                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->u_exc, hc->n_exc,
+                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, gi ? hc->sweep_act[gi - 1] : (int)force, hc->u_exc, hc->n_exc,
                              hc->aug_reached, hc->aug_short);
                 for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
                     const int x = hc->dbg_x[k];
@@ -4727,14 +4722,36 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             int last = 0;
             for (int k = 0; k < gi; ++k)
                 if (hc->sweep_act[k]) last = k + 1;
-            if (!hc->sweep_act[gi - 1]) {
+            if (gi > 0 && !hc->sweep_act[gi - 1]) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
+            }
+            if (force) {   // the forced tail: updates and unlimited walks, no sweeps
+                if (hc->n_exc == 0) break;   // the flow is feasible
+                force_stall = (force_units >= 0 && hc->u_exc >= force_units) ? force_stall + 1 : 0;
+                force_units = hc->u_exc;
+                if (force_stall >= 3) {   // no progress: the phase's own sweeps finish it
+                    force = false;
+                    wsl = walk_sl;
+                    gi = gi_tail;
+                }
+                list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
+                cur ^= 1;
+                continue;
             }
             phase_peak = std::max(phase_peak, hc->n_exc);
             if (may_end_early && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
+            }
+            if (force_tail && hc->n_exc <= kForceNodes && (long long)hc->n_exc * phase_frac <= phase_peak) {
+                force = true;
+                wsl = force_sl;
+                gi = 0;
+                fwd = 0;
+                list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
+                cur ^= 1;
+                continue;
             }
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
@@ -4977,7 +4994,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // (ε > 1): a phase at ε = 1 must end 1-optimal (fault_inject bit 0 breaks
         // exactly this, for the certificate-recovery test)
         const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
-        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl);
+        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl, prc_now);
         if (rc == KS_E_INFEASIBLE) {
             status = rc;
             break;

@@ -62,7 +62,10 @@ int main(int argc, char** argv) {
                 }
         int64_t qh = 0, qt = 0, qn = 0;
         for (int64_t v = 0; v < n; ++v) { cur[v] = r.first[v]; inq[v] = 0; if (r.ex[v] > 0) { q[qt++] = v; inq[v] = 1; ++qn; } }
+        const int64_t EARLY = getenv("CC_EARLY") ? atoll(getenv("CC_EARLY")) : 0;   /* last phase ends at <= EARLY excess nodes */
+        const int lastc = !(eps > efin * STOP * 8);   /* the phase PRC follows */
         while (qn > 0) {
+            if (EARLY && lastc && qn <= EARLY) break;
             int64_t u = q[qh++]; if (qh == n + 1) qh = 0; --qn; inq[u] = 0;
             while (r.ex[u] > 0) {
                 int64_t a = cur[u];
@@ -82,6 +85,42 @@ int main(int argc, char** argv) {
                     if (r.rcap[b] > 0) { int64_t rc = r.cost[b] + p[u] - p[r.head[b]]; if (rc < mn) mn = rc; }
                 p[u] -= mn + eps;
                 cur[u] = r.first[u];
+            }
+        }
+        {   /* forced routing of what an early end left: Dijkstra on max(0, rc) from each excess node */
+            int64_t left = 0, nx = 0;
+            for (int64_t v = 0; v < n; ++v) if (r.ex[v] > 0) { left += r.ex[v]; ++nx; }
+            if (left) {
+                int64_t* dd = malloc(8 * n); int64_t* pa = malloc(8 * n); char* done = calloc(n, 1);
+                int64_t* hk = malloc(16 * m + 16); int64_t* hv = malloc(16 * m + 16);
+                int64_t routed = 0;
+                for (int64_t s0 = 0; s0 < n; ++s0) {
+                    while (r.ex[s0] > 0) {
+                        for (int64_t v = 0; v < n; ++v) { dd[v] = INF; pa[v] = -1; done[v] = 0; }
+                        /* simple binary heap */
+                        int64_t hn = 0; dd[s0] = 0; hk[hn] = 0; hv[hn++] = s0;
+                        int64_t t = -1;
+                        while (hn) {
+                            int64_t bi = 0; for (int64_t i = 1; i < hn; ++i) if (hk[i] < hk[bi]) bi = i;   /* O(n) pop: prototype */
+                            int64_t k0 = hk[bi], u = hv[bi]; hk[bi] = hk[--hn]; hv[bi] = hv[hn];
+                            if (done[u] || k0 > dd[u]) continue;
+                            done[u] = 1;
+                            if (r.ex[u] < 0 && u != s0) { t = u; break; }
+                            for (int64_t a = r.first[u]; a < r.first[u + 1]; ++a) {
+                                if (r.rcap[a] <= 0) continue;
+                                int64_t w = r.head[a], rc = r.cost[a] + p[u] - p[w];
+                                int64_t nd = dd[u] + (rc > 0 ? rc : 0);
+                                if (nd < dd[w]) { dd[w] = nd; pa[w] = a; hk[hn] = nd; hv[hn++] = w; }
+                            }
+                        }
+                        if (t < 0) { fprintf(stderr, "no route\n"); exit(3); }
+                        int64_t dl = r.ex[s0] < -r.ex[t] ? r.ex[s0] : -r.ex[t];
+                        for (int64_t v = t; v != s0; v = tail[pa[v]]) if (r.rcap[pa[v]] < dl) dl = r.rcap[pa[v]];
+                        for (int64_t v = t; v != s0; v = tail[pa[v]]) { r.rcap[pa[v]] -= dl; r.rcap[r.rev[pa[v]]] += dl; }
+                        r.ex[s0] -= dl; r.ex[t] += dl; routed += dl;
+                    }
+                }
+                printf("  forced routing: %lld units from %lld excess nodes\n", (long long)routed, (long long)nx);
             }
         }
         int64_t c = 0;
