@@ -391,7 +391,10 @@ def run_incremental(args, D):
     and checks every round's cost and flow against it (outside the timed region)."""
     T, M, R, J, seed = gen.CONFIGS["config3"]
     cell = churn.Cell(T, M, R, J, seed + D.rank)
-    ctx = native.Context(D.local, **dict(opts_of(args), warm_start=args.warm))
+    # --warm unset: the library's default re-solve mode (from scratch, warm_start 0:
+    # the lower worst round in the round-5 interleaved A/B, DESIGN §5)
+    wopt = {} if args.warm is None else {"warm_start": args.warm}
+    ctx = native.Context(D.local, **dict(opts_of(args), **wopt))
     g = cell.graph()
     ctx.load_graph(g)
     r0 = ctx.solve()
@@ -494,7 +497,7 @@ def run_incremental(args, D):
                                                                  "in-repo single-threaded cost-scaling oracle"}}
     config = {"workload": f"config4: config-3 cell (T={T} M={M}) under churn, {done} completions + "
                           f"{arrive} arrivals per round, pins/ageing/capacity deltas; step = apply deltas + "
-                          f"{'warm-started' if args.warm else 'from-scratch'} re-solve + mapping; {args.steps} timed "
+                          f"{'warm-started' if any(x['warm'] for x in timed) else 'from-scratch'} re-solve + mapping; {args.steps} timed "
                           f"rounds after {args.warmup}", "tasks": T, "machines": M, "seed": seed,
               "initial_solve_ms": round(r0.raw["ms"]["total"], 3), "rounds": args.steps,
               "round_ms": {"median": round(float(np.median([x["ms"] for x in timed])), 3),
@@ -664,7 +667,8 @@ def main():
     ap.add_argument("--graphs", type=int, default=64)
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--batch-mode", default="abi", choices=["abi", "union", "streams"])
-    ap.add_argument("--warm", type=int, default=0, help="incremental workload: warm-start re-solves")
+    ap.add_argument("--warm", type=int, default=None,
+                    help="incremental workload: ks_opts.warm_start of the re-solves (default: the library's)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-reps", type=int, default=5, help="CPU baseline: median of this many after 1 warm-up")
     ap.add_argument("--alpha", type=int, default=0)

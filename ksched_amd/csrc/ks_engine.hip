@@ -2543,8 +2543,12 @@ __global__ void k_pr_apply(DG g, int packed) {
 // The refinement then continues; once its frontier drains, every residual arc
 // meets d(u) ≤ d(v) + len(u, v): the prices p − d certify the flow optimal.
 constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
-constexpr int CYC_WALK = 1 << CYC_LOG;
-constexpr int kForceNodes = 64;   // the forced tail of the phase before the finish starts at this many excess nodes
+[[maybe_unused]] constexpr int CYC_WALK = 1 << CYC_LOG;
+#ifndef KS_CYC_EVERY
+#define KS_CYC_EVERY 16
+#endif
+constexpr int CYC_EVERY = KS_CYC_EVERY;   // refinement rounds between parent-graph searches
+constexpr int CYC_PERIODS = 3;            // rounds + search periods per host check
 
 // The parent of every node (itself for a root) from its key's position a (the
 // parent v is the head of a's reverse); its own id as the window minimum; the
@@ -2553,6 +2557,7 @@ template <bool CP>
 __global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* __restrict__ M,
                           int* __restrict__ onc, int* __restrict__ R, long long* __restrict__ gsum,
                           long long* __restrict__ gcap, int* __restrict__ gbad) {
+    if (g.ctl->bf_done) return;   // the refinement converged: no search
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         const long long a = atom_load(&g.dist[ni(u)]) & PK_NONE;
         int v = (int)u;
@@ -2568,8 +2573,9 @@ __global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* 
     }
 }
 // one doubling step: 2^k → 2^(k+1) steps ahead, and the least id over them
-__global__ void k_cyc_dbl(int n, const int* __restrict__ Ji, const int* __restrict__ Mi, int* __restrict__ Jo,
-                          int* __restrict__ Mo) {
+__global__ void k_cyc_dbl(int n, const int* __restrict__ done, const int* __restrict__ Ji,
+                          const int* __restrict__ Mi, int* __restrict__ Jo, int* __restrict__ Mo) {
+    if (*done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
         const int j = Ji[u];
         Jo[u] = Ji[j];
@@ -2578,7 +2584,9 @@ __global__ void k_cyc_dbl(int n, const int* __restrict__ Ji, const int* __restri
 }
 // every node CYC_WALK steps ahead of some node lies on a cycle (the refinement's
 // parent chains are far shorter than CYC_WALK); roots (their own parent) are skipped
-__global__ void k_cyc_mark(int n, const int* __restrict__ JK, const int* __restrict__ J0, int* __restrict__ onc) {
+__global__ void k_cyc_mark(int n, const int* __restrict__ done, const int* __restrict__ JK,
+                           const int* __restrict__ J0, int* __restrict__ onc) {
+    if (*done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
         const int x = JK[u];
         if (J0[x] != x) onc[x] = 1;
@@ -2592,6 +2600,7 @@ template <bool CP>
 __global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
                             const int* __restrict__ R, long long* __restrict__ gsum, long long* __restrict__ gcap,
                             int* __restrict__ gbad) {
+    if (g.ctl->bf_done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         if (!onc[u] || J0[u] == (int)u) continue;
         const int m = MK[u], mn = MK[J0[u]];
@@ -2613,6 +2622,7 @@ template <bool CP>
 __global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
                            const int* __restrict__ R, const long long* __restrict__ gsum,
                            const long long* __restrict__ gcap, const int* __restrict__ gbad, int seq) {
+    if (g.ctl->bf_done) return;
     const Front F = g.bf[seq % 3];
     int out = 0, cyc = 0;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
@@ -4491,35 +4501,43 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(set_eps(1));
         KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, sizeof(int), st));
         hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, 2);
+        const int* done = &s.ctl.p->bf_done;
+        // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
+        // their least id, every good negative one cancelled in parallel (each kernel
+        // returns at once when the refinement has converged)
+        auto search = [&]() {
+            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad);
+            for (int d = 0; d < CYC_LOG; ++d) {
+                if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Jb, Mb, Ja, Ma);
+                else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Ja, Ma, Jb, Mb);
+            }
+            const int* JK = (CYC_LOG & 1) ? Jb : Ja;
+            const int* MK = (CYC_LOG & 1) ? Mb : Ma;
+            hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, done, JK, (const int*)J0, onc);
+            KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
+                   gbad);
+            KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
+                   (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
+        };
+        // batches of CYC_PERIODS × (CYC_EVERY rounds + a search) per host check
         int used = 0, ok = 0;
         for (int batch = 0; used < cap; ++batch) {
-            const int k = std::min(batch == 0 ? 32 : 16, cap - used);
             KS_CHECK(hipEventRecord(s.kev[0], st));
-            bf_rounds(2, k, batch == 0);
+            for (int per = 0; per < (batch == 0 ? 1 : CYC_PERIODS) && used < cap; ++per) {
+                const int k = std::min(batch == 0 ? 2 * CYC_EVERY : CYC_EVERY, cap - used);
+                bf_rounds(2, k, batch == 0);
+                used += k;
+                search();
+                ++prc_searches;
+            }
             KS_CHECK(hipEventRecord(s.kev[1], st));
-            used += k;
+            cp_dirty = cpv;
             KS_CHECK(read_ctl());
             ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
             if (s.h_ctl->bf_done) {
                 ok = 1;
                 break;
             }
-            // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
-            // their least id, every good negative one cancelled in parallel
-            ++prc_searches;
-            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad);
-            for (int d = 0; d < CYC_LOG; ++d) {
-                if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Jb, Mb, Ja, Ma);
-                else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, Ja, Ma, Jb, Mb);
-            }
-            const int* JK = (CYC_LOG & 1) ? Jb : Ja;
-            const int* MK = (CYC_LOG & 1) ? Mb : Ma;
-            hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, JK, (const int*)J0, onc);
-            KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
-                   gbad);
-            KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
-                   (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
-            cp_dirty = cpv;
         }
         if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g, 1);
         KS_CHECK(hipEventRecord(s.ev[7], st));
@@ -4541,13 +4559,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // nodes left for the next, finer one. walk_sl: the tail walks' slack (1 when the
     // phase must end ε-optimal at ε = 1). Returns KS_OK, KS_E_INFEASIBLE (status),
     // or a device / convergence error.
-    // force_tail: the phase the cycle-cancelling finish follows. Once ≤ kForceNodes
-    // nodes hold excess, its tail is routed by the walks alone with no reduced-cost
-    // limit (down the updates' distances, so along near-shortest paths): the flow
-    // becomes feasible in a few updates instead of the tail's dozens, and the few
-    // negative cycles this leaves are cancelled with the others.
-    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl,
-                         bool force_tail = false) -> int {
+    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl) -> int {
         KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
         KS_HOT(cpv, k_saturate, fgrid, BLK, st, g, sat_thr);
@@ -4560,11 +4572,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int fwd = 0;          // the next cycle is a forward tail update (≤ fwd_k excess nodes left)
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
         int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
-        bool force = false;   // the forced tail is running (force_tail)
-        int wsl = walk_sl;    // the walks' slack (unlimited while forced)
-        int force_stall = 0;
-        long long force_units = -1;
-        const int force_sl = (int)std::min<long long>(1LL << 30, (1LL << 61) / std::max<long long>(1, eps_ph));
+        const int wsl = walk_sl;
         int rc = KS_OK;
         // Forward cycle: nupd × [init (or continue the pending search)][kf rounds][apply]
         // [trace][end], then the cycle end; no sweeps (the trace routes the units). An
@@ -4703,7 +4711,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             if (cycle_log) {
                 std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d units %lld n_exc %d walks %d/%d",
-                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, gi ? hc->sweep_act[gi - 1] : (int)force, hc->u_exc, hc->n_exc,
+                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->u_exc, hc->n_exc,
                              hc->aug_reached, hc->aug_short);
                 for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
                     const int x = hc->dbg_x[k];
@@ -4722,37 +4730,16 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             int last = 0;
             for (int k = 0; k < gi; ++k)
                 if (hc->sweep_act[k]) last = k + 1;
-            if (gi > 0 && !hc->sweep_act[gi - 1]) {
+            if (!hc->sweep_act[gi - 1]) {
                 sweeps -= gi - last;
                 break;   // no excess left: refine done
-            }
-            if (force) {   // the forced tail: updates and unlimited walks, no sweeps
-                if (hc->n_exc == 0) break;   // the flow is feasible
-                force_stall = (force_units >= 0 && hc->u_exc >= force_units) ? force_stall + 1 : 0;
-                force_units = hc->u_exc;
-                if (force_stall >= 3) {   // no progress: the phase's own sweeps finish it
-                    force = false;
-                    wsl = walk_sl;
-                    gi = gi_tail;
-                }
-                list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
-                cur ^= 1;
-                continue;
             }
             phase_peak = std::max(phase_peak, hc->n_exc);
             if (may_end_early && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
-            if (force_tail && hc->n_exc <= kForceNodes && (long long)hc->n_exc * phase_frac <= phase_peak) {
-                force = true;
-                wsl = force_sl;
-                gi = 0;
-                fwd = 0;
-                list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
-                cur ^= 1;
-                continue;
-            }
+
             gi = (use_aug && hc->n_exc <= g.aug_k) ? gi_tail : gi_base;
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
             // forward tail updates only in coarse phases: in the last phase config 3's
@@ -4994,7 +4981,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // (ε > 1): a phase at ε = 1 must end 1-optimal (fault_inject bit 0 breaks
         // exactly this, for the certificate-recovery test)
         const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
-        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl, prc_now);
+        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl);
         if (rc == KS_E_INFEASIBLE) {
             status = rc;
             break;
