@@ -147,7 +147,6 @@ def roofline_of(results, workload: str):
         # L2, so 24 B per unit is not HBM traffic. Its HBM line is the PMC counter bytes
         # (FETCH_SIZE + WRITE_SIZE per launch) over this run's event-timed launch, and its
         # compute line the VALU issue rate of the same profile (2 wave64 VALU per CU-cycle).
-        line["achieved_algorithmic_24B"] = line["achieved"]
         line["bytes_per_unit"] = None
         line["bytes_per_launch"] = None
         raw = k.get("raw_bytes_per_launch")
