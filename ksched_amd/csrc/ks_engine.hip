@@ -2549,6 +2549,10 @@ constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
 #endif
 constexpr int CYC_EVERY = KS_CYC_EVERY;   // refinement rounds between parent-graph searches
 constexpr int CYC_PERIODS = 3;            // rounds + search periods per host check
+#ifndef KS_PRC_UNITS_DIV
+#define KS_PRC_UNITS_DIV 4
+#endif
+constexpr long long kPrcUnitsDiv = KS_PRC_UNITS_DIV;   // an earlier finish (run_phase prc_early)
 
 // The parent of every node (itself for a root) from its key's position a (the
 // parent v is the head of a's reverse); its own id as the window minimum; the
@@ -4484,6 +4488,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // graph that cancels the negative cycles it holds. 1 = certified (prices set),
     // 0 = gave up within cap rounds (the final cost-scaling phase follows), < 0 error.
     int prc_cycles = 0, prc_searches = 0;
+    long long solve_units = -1;   // excess units at the solve's first update (cold: the supply)
     auto prc_refine = [&](int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(s.cyc.ensure((size_t)8 * nn));
@@ -4559,7 +4564,13 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // nodes left for the next, finer one. walk_sl: the tail walks' slack (1 when the
     // phase must end ε-optimal at ε = 1). Returns KS_OK, KS_E_INFEASIBLE (status),
     // or a device / convergence error.
-    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl) -> int {
+    // prc_early: when non-null, the phase may turn itself into the one the cycle-
+    // cancelling finish follows (*prc_early = 1, the phase then drains): at its first
+    // update, if at most 1/KS_PRC_UNITS_DIV of the solve's first-update units hold
+    // excess — the flow is already close to optimal (config 4's churn
+    // rounds, 0.07–0.11 of the supply, vs ≥ 1.9 for cold configs 2 and 3)
+    auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl,
+                         int* prc_early = nullptr) -> int {
         KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
         KS_HOT(cpv, k_saturate, fgrid, BLK, st, g, sat_thr);
@@ -4573,6 +4584,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int fwd_block = 0;    // a forward cycle failed or moved nothing: the next one is a backward update
         int fwd_budget = 64;  // rounds a forward search may take: twice the last global update's
         const int wsl = walk_sl;
+        bool early = may_end_early;
+        bool first_upd = true;
         int rc = KS_OK;
         // Forward cycle: nupd × [init (or continue the pending search)][kf rounds][apply]
         // [trace][end], then the cycle end; no sweeps (the trace routes the units). An
@@ -4721,6 +4734,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
                 std::fprintf(stderr, "\n");
             }
+            if (first_upd) {
+                first_upd = false;
+                if (solve_units < 0) solve_units = hc->u_exc;
+                if (prc_early && early && hc->u_exc * kPrcUnitsDiv <= solve_units) {
+                    early = false;
+                    *prc_early = 1;
+                }
+            }
             kb = std::max(kb_min, std::min(256, hc->bf_count - hc->bf_r0 + kb_margin));
             fwd_budget = std::max(16, 2 * (hc->bf_count - hc->bf_r0));
             ++gus;
@@ -4735,7 +4756,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 break;   // no excess left: refine done
             }
             phase_peak = std::max(phase_peak, hc->n_exc);
-            if (may_end_early && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
+            if (early && hc->n_exc <= phase_exit && (long long)hc->n_exc * phase_frac <= phase_peak) {
                 ++early_exits;
                 break;   // a coarse phase: the next one absorbs the few units left
             }
@@ -4744,7 +4765,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             list = g.bound && hc->n_exc > 0 && hc->n_exc <= BX_CAP;
             // forward tail updates only in coarse phases: in the last phase config 3's
             // searches reach the cluster aggregator and widen
-            fwd = use_fwd && may_end_early && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
+            fwd = use_fwd && early && !fwd_block && hc->n_exc > 0 && hc->n_exc <= fwd_k;
             fwd_block = 0;
             if (phase_sweeps > (uint64_t)(64 * ((uint64_t)nn + 64)) || wall_s() > kSolveWallLimitS) {
                 (void)hipStreamSynchronize(st);
@@ -4977,20 +4998,27 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         const bool before_last = !last_phase && !prc_tried &&
                                  (eps_next / alpha < 1 || eps_next <= 1 || (use_pr && eps_next * pr_div < mult));
         const bool prc_now = use_prc && before_last;
+        // two phases before the last: the finish may follow this phase instead
+        // (run_phase prc_early) when the flow is already close to optimal
+        const long long eps_next2 = std::max<long long>(1, eps_next / alpha);
+        const bool before_last2 = !last_phase && !before_last &&
+                                  (eps_next2 / alpha < 1 || eps_next2 <= 1 || (use_pr && eps_next2 * pr_div < mult));
         // walk slack > 1 only while a finer phase or price refinement still follows
         // (ε > 1): a phase at ε = 1 must end 1-optimal (fault_inject bit 0 breaks
         // exactly this, for the certificate-recovery test)
         const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
-        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl);
+        int prc_early = 0;
+        const bool may_early = use_prc && !prc_tried && before_last2 && !use_warm && !fb;
+        const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl, may_early ? &prc_early : nullptr);
         if (rc == KS_E_INFEASIBLE) {
             status = rc;
             break;
         }
         if (rc) return rc;
-        if (prc_now) {   // the feasible flow of the last coarse phase: cancel its negative cycles
+        if (prc_now || prc_early) {   // the feasible flow of the last coarse phase: cancel its negative cycles
             prc_tried = true;
             int used = 0;
-            const int pr = prc_refine(&used, prc_cap);
+            const int pr = prc_refine(&used, prc_early ? std::min(prc_cap, 1024) : prc_cap);
             if (pr < 0) return pr;
             if (pr == 1) {
                 eps = 1;
