@@ -173,7 +173,7 @@ int ks_abi_version(void) { return KSMCMF_ABI_VERSION; }
 void ks_default_opts(ks_opts* o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
-    o->alpha = 8;
+    o->alpha = 0;   // the library's size-dependent default (ks_engine.hip)
     o->verify = 1;
     o->auto_sink = 1;
     o->price_refine = 1;

@@ -34,7 +34,7 @@ def test_abi_version_and_default_opts():
     lib = native.load()
     assert lib.ks_abi_version() == native.ABI_VERSION == 4
     o = native.default_opts()
-    assert (o.alpha, o.verify, o.auto_sink) == (8, 1, 1)
+    assert (o.alpha, o.verify, o.auto_sink) == (0, 1, 1)   # alpha 0: the size-dependent default
     assert o.price_refine == 1 and o.gu_interval > 0 and o.warm_start == 0
     assert o.cell_nodes == 0   # the cell solver on by default for graphs its LDS holds
 

@@ -317,7 +317,8 @@ def test_tail_updates_do_not_change_the_optimum(opts):
     tail), and down to ε = 1 without price refinement; the bounded global update
     off. Same optimum as the oracle, flow re-verified, on a config-2-sized cell
     and random graphs (several deficits, lower bounds, parallel paths)."""
-    with native.Context(0, cell_nodes=-1, **opts) as c2:   # the engine's tail updates
+    # α 8: a config-2 solve at its default α (16) has no coarse phase with a tail
+    with native.Context(0, cell_nodes=-1, alpha=8, **opts) as c2:   # the engine's tail updates
         g = gen.quincy(10_000, 1_000, 25, 100, 2)
         st, c, fv, _, _ = ko.ssp(g)
         assert st == 0
