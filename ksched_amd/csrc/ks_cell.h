@@ -68,22 +68,26 @@ struct CellOut {
     int pr_ok;             // price refinements that certified the flow
     int pr_tries;
     int last_eps;          // 1 when the solve ended at ε = 1 (scaled)
-    int pad[2];
+    int cycles;            // negative cycles the cycle-cancelling finish cancelled
+    int searches;          // its parent-graph searches
+    unsigned cyc_dbg[4];   // diagnostics: nodes with a parent, marked on a cycle, leaders, closed walks
     unsigned long long sweeps, bf_rounds, scans, visits, pushes, relabels, gu_scans;
     unsigned long long ticks;   // s_memrealtime ticks (100 MHz) of the cell's solve
     // per operation kind (saturate, update init, Bellman-Ford round, update apply,
     // sweep, refinement init, refinement round, refinement apply): ticks incl. the
     // barriers and the controller, and counts
-    unsigned long long op_ticks[8];
-    unsigned op_n[8];
-    unsigned long long item_ticks[8];    // diagnostics: op start → the last wave's items done
-    unsigned long long first_ticks[8];   //              op start → the first wave's items done
+    unsigned long long op_ticks[9];      // (and the finish's parent-graph searches)
+    unsigned op_n[9];
+    unsigned long long item_ticks[9];    // diagnostics: op start → the last wave's items done
+    unsigned long long first_ticks[9];   //              op start → the first wave's items done
     unsigned long long cls_ticks[32];    //              item ticks by step (sweep, BF, refinement, saturate) × class
     unsigned cls_n[32];                  //              and items (class 6: the workgroup-sized nodes)
     unsigned long long hist_t[12];       //              sweep (0–5) / BF round (6–11) ticks by frontier size
     unsigned hist_n[12];                 //              (≤ 16, 64, 256, 1k, 4k, more nodes) and counts
+    unsigned long long phase_ticks[8];   //              ticks by ε-phase (the last slot: phases 8 and up,
+                                         //              and the refinements)
 };
-constexpr int CELL_NOPS = 8;
+constexpr int CELL_NOPS = 9;
 
 struct CellArgs {
     Pos* pos;
@@ -107,6 +111,8 @@ struct CellArgs {
     int pr_div;              // price refinement once ε·pr_div < mult
     int use_pr;
     int pr_cap;              // Bellman-Ford rounds a price refinement may take
+    int use_prc;             // the cycle-cancelling finish (ks_opts.price_refine 1)
+    int prc_cap;             // its rounds before it gives up (the final phase then runs)
     int gi;                  // sweeps between global updates
     int phase_exit, phase_frac;   // coarse phases end with few excess nodes left
     int mode;                // 0: solve from the state in place; 1: certificate recovery at ε = 1

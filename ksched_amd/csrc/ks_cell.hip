@@ -52,6 +52,16 @@ constexpr long long DCAP = 1LL << 30;      // distances saturate here
 constexpr long long DNEG = -(1LL << 30);   // price refinement below this: treated as a negative cycle
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr int BXC = 256;                   // updates with at most this many excess nodes are bounded
+// cycle-cancelling finish (cyc_search)
+constexpr int CYC_LOG = 10;                 // cycles of up to 1,024 arcs
+constexpr int CYC_WALK = 1 << CYC_LOG;
+#ifndef KS_CELL_CYC_EVERY
+#define KS_CELL_CYC_EVERY 16
+#endif
+constexpr int CYC_EVERY = KS_CELL_CYC_EVERY;   // refinement rounds between searches
+constexpr int CYC_IDB = 15;                 // bits of a local node id in the packed word (cells ≤ 32k nodes)
+constexpr int CYC_IDM = (1 << CYC_IDB) - 1;
+constexpr int CYC_ON = 1 << 30;             // marked: on a cycle
 
 enum { OP_SWEEP = 0, OP_BF = 1, OP_PR = 2, OP_SAT = 3 };
 enum { F_INFEAS = 1, F_NEG = 2 };
@@ -86,6 +96,7 @@ struct K {
     int eps_shift;        // log2 ε when ε is a power of two (the cell ladder's are), else −1
     int sp;               // sweep parity (pending-relabel buffer)
     int bnd;              // s_.bnd at the step's start
+    int prc;              // the refinement records parents (the cycle-cancelling finish)
 };
 
 // Work counters (ks_result units): counted per lane in registers, summed over the
@@ -535,6 +546,19 @@ __device__ __forceinline__ void sweep_hub(const CellArgs& A, K& k, int nb, int v
 // In-arc (u → v) = the reverse of v's position a; its residual is ucap − rcap
 // and its reduced cost −(cost(a) + p(v) − p(u)). PR: price refinement (ε = 1,
 // negative lengths allowed, no clamp at 0).
+// the finish's parent keys: offer (biased into 32 bits) above the parent arc's position
+constexpr unsigned long long PKEY_NONE = ~0ULL;
+__device__ __forceinline__ unsigned long long pkey(long long d, int a) {
+    return ((unsigned long long)(d + (1LL << 31)) << 32) | (unsigned)a;   // d in [DNEG, DCAP]
+}
+__device__ __forceinline__ int key_pos(unsigned long long k) {
+    return k == PKEY_NONE ? -1 : (int)(unsigned)(k & 0xffffffffULL);
+}
+// (the keys change only by atomics, performed in L2: read them there, not from L1)
+__device__ __forceinline__ int key_at(const unsigned long long* key, int l) {
+    return key_pos(__hip_atomic_load(key + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 template <bool PR>
 __device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, const Pos& q, int dv, long long pv) {
     if (q.ucap - q.rcap <= 0) return;
@@ -567,7 +591,13 @@ __device__ __forceinline__ void relax_q(const CellArgs& A, const K& k, int nb, c
     }
     if (cand < (long long)D[lu]) {
         const int old = atomicMin(&D[lu], (int)cand);
-        if (cand < (long long)old) mark(A, k, nb, q.head);
+        if (cand < (long long)old) {
+            mark(A, k, nb, q.head);
+            // the parent arc (head → v, the reverse of q) for the finish's cycle search:
+            // the least offer's, as the engine's packed keys (a 64-bit key in global
+            // memory, offer above the position: the minimum is the final distance's arc)
+            if (k.prc) atomicMin(reinterpret_cast<unsigned long long*>(A.rl_p) + q.head, pkey(cand, q.rev));
+        }
     }
 }
 
@@ -1037,7 +1067,7 @@ __device__ __forceinline__ void step_post(const CellArgs& A, const K& k, int src
 // the device), and the whole workgroup executes one operation per iteration of
 // the kernel's loop. Every operation starts and ends at a barrier, so no
 // register state lives across operations.
-enum Op { O_SAT, O_GUINIT, O_BF, O_GUFIN, O_SWEEP, O_PRINIT, O_PR, O_PRFIN, O_DONE };
+enum Op { O_SAT, O_GUINIT, O_BF, O_GUFIN, O_SWEEP, O_PRINIT, O_PR, O_PRFIN, O_CYC, O_DONE };
 enum Next { N_PHASE_LOOP = 0, N_RECOVERY = 1 };
 
 struct Ctl {
@@ -1049,6 +1079,10 @@ struct Ctl {
     int phases, pr_failed, early, status;
     int peak, cyc_sweeps, upd_rounds, pr_rounds, pr_cap, pr_ok_now, pr_next, nexc;
     int updates, pr_ok, pr_tries, ended_at_one;
+    int drain;                // this phase drains: the cycle-cancelling finish follows it
+    int prc, prc_tried;       // the finish's refinement is running / was tried
+    int cycles, searches;     // cycles it cancelled, parent-graph searches
+    unsigned cyc_dbg[4];
     unsigned long long phase_sweeps, sweeps, rounds;
     unsigned long long t_op;                // when the running operation started
     unsigned long long op_ticks[O_DONE];    // 100 MHz ticks per operation kind (incl. its barriers)
@@ -1058,12 +1092,20 @@ struct Ctl {
     int fsz;                                // diagnostics: the running step's frontier size
     unsigned long long hist_t[12];          //              sweep / BF ticks by frontier size (≤16, 64, 256, 1k, 4k, more)
     unsigned hist_n[12];
+    unsigned long long phase_ticks[8];      //              ticks by phase (slot 7: later phases, refinements)
+    unsigned long long t_phase;             //              when the running phase (or refinement) began
 };
 __shared__ Ctl c_;
 
 __device__ __forceinline__ int total_any(int src) { return total_of(src); }
 
 // thread 0 only: a phase of ε = eps_ph begins (DESIGN §3 ε schedule)
+__device__ __forceinline__ void phase_tick(unsigned long long now) {   // diagnostics
+    Ctl& c = c_;
+    const int slot = c.op == O_PR || c.op == O_PRINIT || c.op == O_PRFIN ? 7 : min(7, max(0, c.phases - 1));
+    c.phase_ticks[slot] += now - c.t_phase;
+    c.t_phase = now;
+}
 __device__ __forceinline__ void begin_phase(const CellArgs& A) {
     Ctl& c = c_;
     ++c.phases;
@@ -1071,6 +1113,12 @@ __device__ __forceinline__ void begin_phase(const CellArgs& A) {
     c.pr_failed = 0;
     const bool last = c.eps_ph / A.alpha < 1 || c.eps_ph <= 1 || (A.use_pr && c.eps_ph * A.pr_div < A.mult);
     c.early = last ? 0 : 1;
+    // the phase before the last drains when the cycle-cancelling finish replaces the
+    // last one
+    const long long nx = c.eps_ph / A.alpha > 1 ? c.eps_ph / A.alpha : 1;
+    const bool before_last = !last && (nx / A.alpha < 1 || nx <= 1 || (A.use_pr && nx * A.pr_div < A.mult));
+    c.drain = A.use_prc && before_last && !c.prc_tried;
+    if (c.drain) c.early = 0;
     c.eps = c.eps_ph;
     c.peak = 0;
     c.phase_sweeps = 0;
@@ -1085,6 +1133,15 @@ __device__ __forceinline__ void finish(int status) {
 // after a phase: price refinement where it may certify, then the next phase
 __device__ __forceinline__ void phase_end(const CellArgs& A) {
     Ctl& c = c_;
+    if (c.drain) {   // the drained flow: refinement with parents, cancelling the cycles it meets
+        c.drain = 0;
+        c.prc_tried = 1;
+        c.prc = 1;
+        c.op = O_PRINIT;
+        c.pr_cap = A.prc_cap;
+        c.pr_next = N_PHASE_LOOP;
+        return;
+    }
     if (A.use_pr && c.eps_ph > 1 && c.eps_ph * A.pr_div < A.mult) {
         c.op = O_PRINIT;
         c.pr_cap = A.pr_cap;
@@ -1127,6 +1184,7 @@ __device__ __forceinline__ void control_body(const CellArgs& A, int N, unsigned 
     t_first_ = ~0ULL;
     c.t_op = now;
     if (now - c.t0 > A.timeout_ticks) return finish(CS_TIMEOUT);
+    if (A.diag) phase_tick(now);
     // TESTS ONLY: one cell gives up part-way, as a step cap would (the host then
     // re-solves that cell alone on the engine)
     if ((int)blockIdx.x == A.fault_cell) {
@@ -1198,11 +1256,17 @@ __device__ __forceinline__ void control_body(const CellArgs& A, int N, unsigned 
             else {
                 c.src = c.nb;
                 c.nb ^= 1;
+                if (c.prc && c.pr_rounds % CYC_EVERY == 0) c.op = O_CYC;   // not converged yet: search
                 return;
             }
             c.op = O_PRFIN;
             return;
+        case O_CYC:
+            ++c.searches;
+            c.op = O_PR;
+            return;
         case O_PRFIN:
+            c.prc = 0;
             c.eps = c.eps_ph;
             if (c.pr_ok_now) ++c.pr_ok;
             if (c.pr_next == N_RECOVERY) {
@@ -1301,6 +1365,95 @@ __device__ __forceinline__ void gu_fin(const CellArgs& A, const K& k) {
     if (threadIdx.x == 0) c_.nexc = n;
 }
 
+// ------------------------------------------------ cycle-cancelling finish ---
+// The engine's finish (ks_engine.hip k_cyc_*) inside the workgroup. The
+// phase before the last drains; price refinement from d ≡ 0 then records each
+// improved node's parent arc with its least offer (a 64-bit key per node in rl_p,
+// free while no sweep runs), and every CYC_EVERY rounds that have not converged the
+// parent graph is searched: one word per node packs the node 2^k steps ahead and the
+// least id over those steps (pointer doubling in place, in rl_node's slice, free
+// likewise — a word is read and
+// written whole, so a reader never pairs a new jump with an old minimum); after
+// CYC_LOG steps every node a window ahead of another lies on a cycle (marked), and
+// each cycle's least id walks it — its arcs residual, every node agreeing on the
+// least id (a cycle longer than the window has nodes that disagree), the cost
+// negative — and pushes the bottleneck around it. Cycles of the parent graph are
+// node-disjoint (one parent per node), so the walkers never share an arc. The
+// cycle's nodes rejoin the next round's frontier; the refinement certifies once
+// its frontier drains. Giving up (prc_cap rounds) leaves a feasible flow to the
+// final phase.
+
+__device__ __forceinline__ void cyc_search(const CellArgs& A, const K& k, int src, int nb) {
+    // N words each: jump | least id << CYC_IDB, double-buffered (every step reads the
+    // previous step's words only: in place, the jumps of a cycle's nodes can fold onto
+    // one node, and a cycle must be every node's destination to be found)
+    int* Wb[2] = {A.rl_node + k.x0, A.lists + (size_t)nb * A.nn + k.x0};   // (buffer nb is empty until the next round)
+    int* W = Wb[0];
+    const unsigned long long* key = reinterpret_cast<const unsigned long long*>(A.rl_p) + k.x0;
+    unsigned dbg[4] = {0, 0, 0, 0};
+    for (int l = threadIdx.x; l < k.N; l += CT) {
+        const int a = key_at(key, l);
+        const int j = a >= 0 ? ld_cp(A, k, a).head - k.x0 : l;
+        W[l] = j | (l << CYC_IDB);
+        dbg[0] += a >= 0;
+    }
+    __syncthreads();
+    for (int d = 0; d < CYC_LOG; ++d) {
+        const int* Wi = Wb[d & 1];
+        int* Wo = Wb[(d & 1) ^ 1];
+        for (int l = threadIdx.x; l < k.N; l += CT) {
+            const int w = Wi[l];
+            const int wx = Wi[w & CYC_IDM];   // 2^d steps ahead of l, then 2^d more
+            Wo[l] = (wx & CYC_IDM) | (min(w >> CYC_IDB, wx >> CYC_IDB) << CYC_IDB);
+        }
+        __syncthreads();
+    }
+    W = Wb[CYC_LOG & 1];
+    for (int l = threadIdx.x; l < k.N; l += CT) {
+        const int x = W[l] & CYC_IDM;
+        if (key_at(key, x) >= 0 && !(atomicOr(&W[x], CYC_ON) & CYC_ON)) ++dbg[1];
+    }
+    __syncthreads();
+    int found = 0;
+    for (int l = threadIdx.x; l < k.N; l += CT) {
+        const int w = W[l];
+        if (!(w & CYC_ON) || ((w & ~CYC_ON) >> CYC_IDB) != l) continue;
+        ++dbg[2];
+        long long cost = 0;
+        int cap = 0x7fffffff, x = l;
+        bool ok = false;
+        for (int st = 0; st < CYC_WALK; ++st) {
+            const int a = key_at(key, x);
+            if (a < 0) break;
+            const Pos q = ld_cp(A, k, a);
+            const int wx = W[x];
+            if (q.rcap <= 0 || !(wx & CYC_ON) || ((wx & ~CYC_ON) >> CYC_IDB) != l) break;
+            cost += q.cost;
+            cap = min(cap, (int)q.rcap);
+            x = q.head - k.x0;
+            if (x == l) {
+                ok = true;
+                break;
+            }
+        }
+        dbg[3] += ok;
+        if (!ok || cost >= 0) continue;
+        x = l;
+        do {
+            const int a = key_at(key, x);
+            const Pos q = ld_cp(A, k, a);
+            st_rcap(A, a, q.rcap - cap);
+            st_rcap(A, q.rev, q.ucap - (q.rcap - cap));
+            mark(A, k, src, x + k.x0);
+            x = q.head - k.x0;
+        } while (x != l);
+        ++found;
+    }
+    if (found) atomicAdd(&c_.cycles, found);
+    for (int i = 0; i < 4; ++i)
+        if (dbg[i]) atomicAdd(&c_.cyc_dbg[i], dbg[i]);
+}
+
 __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
     const CellDesc cd = A.cells[blockIdx.x];
     const int N = cd.cb[CELL_NCLS] - cd.cb[0];
@@ -1326,6 +1479,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         c = Ctl{};
         c.t0 = __builtin_amdgcn_s_memrealtime();
         c.t_op = c.t0;
+        c.t_phase = c.t0;
         t_items_ = 0;
         t_first_ = ~0ULL;
         for (int i = 0; i < 32; ++i) {
@@ -1383,6 +1537,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         k.eps_shift = (k.eps & (k.eps - 1)) == 0 ? __builtin_ctzll((unsigned long long)k.eps) : -1;
         k.sp = c_.sp;
         k.bnd = s_.bnd;
+        k.prc = c_.prc;
         const int src = c_.src, nb = c_.nb;
         switch (op) {
             case O_SAT:
@@ -1408,11 +1563,17 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
                 int* D = dst(k);
                 reset_lists(k);
                 for (int l = threadIdx.x; l < N; l += CT) D[l] = 0;
+                if (c_.prc)   // no parents yet
+                    for (int l = threadIdx.x; l < N; l += CT)
+                        reinterpret_cast<unsigned long long*>(A.rl_p)[k.x0 + l] = PKEY_NONE;
                 if (threadIdx.x == 0) s_.flag &= ~F_NEG;
                 break;
             }
             case O_PR:
                 step<OP_PR>(A, k, src, nb, 0);
+                break;
+            case O_CYC:
+                cyc_search(A, k, src, nb);
                 break;
             case O_PRFIN:
                 if (c_.pr_ok_now) {
@@ -1453,6 +1614,9 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         o.pr_ok = c.pr_ok;
         o.pr_tries = c.pr_tries;
         o.last_eps = c.ended_at_one;
+        o.cycles = c.cycles;
+        o.searches = c.searches;
+        for (int i = 0; i < 4; ++i) o.cyc_dbg[i] = c.cyc_dbg[i];
         o.sweeps = c.sweeps;
         o.bf_rounds = c.rounds;
         o.scans = ctr_[C_SCAN];
@@ -1475,6 +1639,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
             o.hist_t[i] = c.hist_t[i];
             o.hist_n[i] = c.hist_n[i];
         }
+        for (int i = 0; i < 8; ++i) o.phase_ticks[i] = c.phase_ticks[i];
         A.out[blockIdx.x] = o;
     }
 }

@@ -4852,6 +4852,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         a.pr_div = (int)pr_div;
         a.use_pr = use_pr ? 1 : 0;
         a.pr_cap = pr_cap;
+        a.use_prc = (use_pr && o.price_refine == 1 && !use_warm && mode == 0) ? 1 : 0;
+        a.prc_cap = (o.fault_inject & 32) ? 32 : 4096;
         a.gi = gi_base;
         a.bound = o.bf_bound < 0 ? 0 : 1;
         a.phase_exit = phase_exit;
@@ -4889,6 +4891,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             cell_ctr[2] += o.pushes;
             cell_ctr[3] += o.relabels;
             cell_ctr[4] += o.gu_scans;
+            prc_cycles += o.cycles;
             cticks_max = std::max<unsigned long long>(cticks_max, o.ticks);
             cticks_sum += o.ticks;
         }
@@ -4898,7 +4901,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             for (size_t i = 1; i < s.h_cell_out.size(); ++i)
                 if (s.h_cell_out[i].ticks > s.h_cell_out[w].ticks) w = i;
             const CellOut& o = s.h_cell_out[w];
-            static const char* names[CELL_NOPS] = {"sat", "gu_init", "bf", "gu_fin", "sweep", "pr_init", "pr", "pr_fin"};
+            static const char* names[CELL_NOPS] = {"sat", "gu_init", "bf", "gu_fin", "sweep", "pr_init", "pr", "pr_fin",
+                                                   "cyc"};
             std::fprintf(stderr, "cell %zu of %d: %.3f ms, phases %d updates %d sweeps %llu rounds %llu:", w, ncells,
                          o.ticks / 1e5, o.phases, o.updates, o.sweeps, o.bf_rounds);
             for (int i = 0; i < CELL_NOPS; ++i)
@@ -4914,6 +4918,11 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                         std::fprintf(stderr, " c%d %u x %.2f us", c, o.cls_n[8 * s + c],
                                      o.cls_ticks[8 * s + c] / 100.0 / o.cls_n[8 * s + c]);
             }
+            std::fprintf(stderr, "\n  finish: cycles %d searches %d parents %u marked %u leaders %u closed %u", o.cycles,
+                         o.searches, o.cyc_dbg[0], o.cyc_dbg[1], o.cyc_dbg[2], o.cyc_dbg[3]);
+            std::fprintf(stderr, "\n  ms by phase:");
+            for (int i = 0; i < 8; ++i)
+                if (o.phase_ticks[i]) std::fprintf(stderr, " %s%d %.2f", i == 7 ? "pr/" : "p", i + 1, o.phase_ticks[i] / 1e5);
             static const char* const sz[6] = {"<=16", "<=64", "<=256", "<=1k", "<=4k", ">4k"};
             for (int h = 0; h < 12; ++h) {
                 if (h % 6 == 0) std::fprintf(stderr, "\n  %s by frontier:", h ? "bf" : "sweep");
