@@ -155,17 +155,22 @@ def test_config4_full_size_rounds():
     ageing and capacity refresh, ten rounds through ks_apply_deltas. Every
     round: bit-exact cost vs the cost-scaling oracle on the cell's full graph,
     the oracle's verifier accepts the downloaded flow, and every running task
-    stays on its PU (graph_manager.go:675-720 pinning, :803-813 removal)."""
+    stays on its PU (graph_manager.go:675-720 pinning, :803-813 removal). The
+    churn rounds start close to optimal, so the cycle-cancelling finish follows
+    the third phase instead of the fourth in most of them (the earlier
+    finish)."""
     T, M, R, J, seed = gen.CONFIGS["config3"]
     cell = churn.Cell(T, M, R, J, seed)
     with native.Context(0) as ctx:
         ctx.load_graph(cell.graph())
         ctx.solve()
         mp = ctx.task_mapping()
+        early = 0
         for rnd in range(10):
             d = cell.step(mp, done=T // 20, arrive=T // 20)
             ctx.apply_deltas(d)
             r = ctx.solve()
+            early += r.raw["phases"] <= 3 and r.raw["cycles_cancelled"] >= 0
             g = cell.graph()
             st, cost, flow, _ = ko.cost_scaling(g)
             assert st == 0
@@ -177,6 +182,7 @@ def test_config4_full_size_rounds():
             check_mapping(g, mp)
             run = cell.task_ids(cell.RUN)
             assert all(mp[int(t)] == int(cell.pu[int(t) - cell.TASK0]) for t in run.tolist())
+        assert early >= 5, f"the earlier finish ran in {early} of 10 rounds"
 
 
 def test_config5_full_batch_vs_goldens(ctx):
