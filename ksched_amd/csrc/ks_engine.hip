@@ -4493,6 +4493,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // 0 = gave up within cap rounds (the final cost-scaling phase follows), < 0 error.
     int prc_cycles = 0, prc_searches = 0;
     long long solve_units = -1;   // excess units at the solve's first update (cold: the supply)
+    unsigned long long gu_prev = 0;   // cycle log: Bellman-Ford relaxations counted so far
     auto prc_refine = [&](int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(s.cyc.ensure((size_t)8 * nn));
@@ -4727,9 +4728,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 continue;
             }
             if (cycle_log) {
-                std::fprintf(stderr, "cycle phase %d eps %lld bf %d bf_ms %.3f sw_ms %.3f active %d units %lld n_exc %d walks %d/%d",
-                             phases, eps_ph, hc->bf_count - hc->bf_r0, t_bf, t_sw, hc->sweep_act[gi - 1], hc->u_exc, hc->n_exc,
+                // (diagnostics: the update's relaxations, from the sharded counters)
+                std::vector<unsigned long long> hctr((size_t)CTR_SHARDS * NCTR);
+                KS_CHECK(hipMemcpy(hctr.data(), s.ctr.p, hctr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+                unsigned long long gsc = 0;
+                for (int i = 0; i < CTR_SHARDS; ++i) gsc += hctr[(size_t)i * NCTR + C_GUSCAN];
+                std::fprintf(stderr, "cycle phase %d eps %lld bf %d relax %llu bf_ms %.3f sw_ms %.3f active %d units %lld n_exc %d walks %d/%d",
+                             phases, eps_ph, hc->bf_count - hc->bf_r0, gsc - gu_prev, t_bf, t_sw, hc->sweep_act[gi - 1], hc->u_exc, hc->n_exc,
                              hc->aug_reached, hc->aug_short);
+                gu_prev = gsc;
                 for (int k = 0; k < std::min(4, hc->n_exc); ++k) {
                     const int x = hc->dbg_x[k];
                     int c = 0;
