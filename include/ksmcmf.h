@@ -92,7 +92,7 @@ typedef struct ks_ctx ks_ctx;
 
 typedef struct ks_opts {
     int32_t  alpha;            /* cost-scaling factor per ε-phase; 0 (ks_default_opts):
-                                  8, or 16 for graphs under 32,768 nodes on the
+                                  8, or 32 for graphs under 32,768 nodes on the
                                   multi-kernel engine                                   */
     int32_t  verify;           /* run the on-device verifier after every solve (1)      */
     int32_t  auto_sink;        /* sink demand = −Σ other supplies at solve time (1)     */

@@ -4362,11 +4362,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     const int fwd_k = o.fwd_nodes > 0 ? (int)o.fwd_nodes : (nn < 32768 ? 32 : 64);
     int kf = 16;                        // forward rounds enqueued per cycle (adaptive)
     uint64_t fwd_updates = 0, fs_launches = 0;
-    // α by size: with the cycle-cancelling finish a small engine graph takes fewer,
-    // wider phases (config 2: 17.9 / 18.0 → 16.1 / 15.6 ms at 16; config 3 and the
-    // config-4 rounds are slower at 16, config 3 also at 4 and 32; the cell solver's
-    // ladder is unchanged) — interleaved A/B, DESIGN §5
-    const int alpha = o.alpha >= 2 ? o.alpha : (!s.cell_layout && nn < 32768) ? 16 : 8;
+    // α by size: with the cycle-cancelling finish a small engine graph is best with
+    // one coarse phase and the finish (12 config-2 graphs, median / max ms: α 8 14.6 /
+    // 17.9, 16 14.9 / 16.5, 32 11.6 / 15.4, 48 12.6 / 15.9, 1024 — a single phase at
+    // the final ε — 13.4 / 24.4); config 3 and the config-4 rounds are slower at 16
+    // and 32, and the cell solver's ladder stays at 8 (config 5 36 ms at 32) — DESIGN §3
+    const int alpha = o.alpha >= 2 ? o.alpha : (!s.cell_layout && nn < 32768) ? 32 : 8;
     int gi_base = o.gu_interval > 0 ? o.gu_interval : 24;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
     const int pr_cap = o.pr_rounds > 0 ? o.pr_rounds : 160;  // price-refinement rounds before giving up

@@ -1,0 +1,39 @@
+"""Median solve time of config-2-sized graphs over several seeds, per ks_opts setting
+(round-5 alpha study). Usage: python tools/c2seeds.py "alpha=16" "alpha=1024" ..."""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from ksched_amd import gen, native  # noqa: E402
+
+
+def parse(spec):
+    o = {}
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        o[k] = int(v)
+    return o
+
+
+T, M, R, J, _ = gen.CONFIGS["config2"]
+seeds = [2, 7, 11] + list(range(1000, 1009))
+graphs = [gen.quincy(T, M, R, J, s) for s in seeds]
+for spec in sys.argv[1:]:
+    opts = parse(spec)
+    cells = opts.pop("cell", 0)
+    ms, costs = [], []
+    with native.Context(0, cell_nodes=20000 if cells else -1, **opts) as ctx:
+        for g in graphs:
+            ctx.load_graph(g)
+            ctx.solve()
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                r = ctx.solve()
+                ts.append(1e3 * (time.perf_counter() - t0))
+            ms.append(float(np.median(ts)))
+            costs.append(r.cost)
+    print(f"{spec or 'default':>24}: median {np.median(ms):6.2f} ms, mean {np.mean(ms):6.2f}, max {max(ms):6.2f}; "
+          f"per seed {' '.join(f'{x:.1f}' for x in ms)}; costs {costs[:3]}", flush=True)
