@@ -113,7 +113,9 @@ typedef struct ks_opts {
                                   [4]; < 0 disables the walkers                       */
     int32_t  final_div;        /* the phase price refinement certifies runs at 1/final_div
                                   of a cost unit [20 for cells and graphs under 32,768
-                                  nodes, else 48]; < 0: the plain max|cost|/α^k ladder   */
+                                  nodes, else 24 with the cycle-cancelling finish
+                                  (price_refine 1) and 48 without]; < 0: the plain
+                                  max|cost|/α^k ladder                                  */
     int32_t  pr_rounds;        /* Bellman-Ford rounds one price refinement may take [160] */
     int32_t  phase_exit;       /* a coarse phase ends once ≤ phase_exit nodes hold excess
                                   [256] ... */

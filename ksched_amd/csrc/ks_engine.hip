@@ -4408,11 +4408,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // at 1/48 in none; 1/64 and 1/96 cost more per phase. D = 20 on small graphs and
     // cells (under 32,768 nodes; every cell is): their flow is usually optimal a
     // phase earlier (config 2 26–27 → 20–21 ms, config 5 53–54 → 41–43 ms).
+    // Round 5: with the cycle-cancelling finish the final phase no longer runs, and
+    // D only places the ladder; large graphs take D = 24 — one coarse phase fewer
+    // (config 3: 35.4–36.9 vs 36.6–38.6 ms in interleaved pairs).
     long long eps = std::max<long long>(1, maxc * mult);
     {
         const long long D = o.final_div < 0 ? 0
                             : o.final_div > 0 ? o.final_div
-                            : (s.cell_layout || nn < 32768) ? 20 : 48;
+                            : (s.cell_layout || nn < 32768) ? 20 : (use_pr && o.price_refine == 1 ? 24 : 48);
         if (D > 0 && use_pr && maxc > 0) {
             long long e = std::max<long long>(1, (mult - 1) / D);
             // the cell solver's ladder is powers of two (α = 8): its arc lengths
@@ -5029,7 +5032,9 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // exactly this, for the certificate-recovery test)
         const int walk_sl = (eps > 1 || (o.fault_inject & 1)) ? aug_slack : 1;
         int prc_early = 0;
-        const bool may_early = use_prc && !prc_tried && before_last2 && !use_warm && !fb;
+        // (only from a phase at most two cost units coarse: earlier, the finish has
+        // too many cycles to cancel — config 4 with D = 24 at 2.6 units: 26 vs 20 ms)
+        const bool may_early = use_prc && !prc_tried && before_last2 && !use_warm && !fb && eps <= 2 * mult;
         const int rc = run_phase(eps, sat_thr, !last_phase && !prc_now, walk_sl, may_early ? &prc_early : nullptr);
         if (rc == KS_E_INFEASIBLE) {
             status = rc;
