@@ -20,6 +20,14 @@
 //              flow is tested by PRICE REFINEMENT at ε = 1 (Bellman-Ford on the
 //              difference constraints of 1-optimality); success proves the flow
 //              optimal and ends the solve early.
+//   finish     (default) the final phase is replaced: the phase before it drains,
+//              then the refinement's Bellman-Ford records each node's parent arc
+//              (packed keys) and every 16 rounds the parent graph is searched by
+//              pointer doubling; its negative cycles are cancelled in parallel
+//              until the refinement certifies (k_cyc_*). A near-optimal
+//              flow (config 4's churn rounds) takes the finish a phase earlier.
+//   layout     the solve's hot kernels read 16-B compact positions (CPos + a
+//              reverse array) when the graph's values fit 32 bits (PL<CP>).
 //   frontier   sweeps and Bellman-Ford rounds only touch the ACTIVE frontier:
 //              one flag byte per node (three rotating buffers) plus per-hub
 //              flags. Producers store 1 (idempotent: no counters, no returning
