@@ -4,8 +4,11 @@
 // starting by saturating every arc of negative reduced cost, then alternating a
 // global price update (Bellman-Ford from the deficits over lengths
 // floor(rc/ε)+1, prices p ← p − ε·min(d, L)) with bursts of push/relabel sweeps
-// against a price snapshot; price refinement at ε = 1 certifies optimality.
-// What changes is where it runs:
+// against a price snapshot; price refinement at ε = 1 certifies optimality. By
+// default the final phase is replaced by the engine's cycle-cancelling finish
+// (the phase before it drains; a refinement with parent keys, whose parent
+// graph's negative cycles are found by pointer doubling and cancelled:
+// cyc_search). What changes is where it runs:
 //
 //   control   the phase loop, every decision and every termination test run on
 //             the device; a step (one sweep, one Bellman-Ford round) ends at a
