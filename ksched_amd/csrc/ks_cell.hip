@@ -58,10 +58,7 @@ constexpr int BXC = 256;                   // updates with at most this many exc
 // cycle-cancelling finish (cyc_search)
 constexpr int CYC_LOG = 10;                 // cycles of up to 1,024 arcs
 constexpr int CYC_WALK = 1 << CYC_LOG;
-#ifndef KS_CELL_CYC_EVERY
-#define KS_CELL_CYC_EVERY 16
-#endif
-constexpr int CYC_EVERY = KS_CELL_CYC_EVERY;   // refinement rounds between searches
+constexpr int CYC_EVERY = 16;               // refinement rounds between searches (8 and 32: no better)
 constexpr int CYC_IDB = 15;                 // bits of a local node id in the packed word (cells ≤ 32k nodes)
 constexpr int CYC_IDM = (1 << CYC_IDB) - 1;
 constexpr int CYC_ON = 1 << 30;             // marked: on a cycle

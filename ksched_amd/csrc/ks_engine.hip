@@ -22,7 +22,7 @@
 //              optimal and ends the solve early.
 //   finish     (default) the final phase is replaced: the phase before it drains,
 //              then the refinement's Bellman-Ford records each node's parent arc
-//              (packed keys) and every 16 rounds the parent graph is searched by
+//              (packed keys) and every 8 rounds the parent graph is searched by
 //              pointer doubling; its negative cycles are cancelled in parallel
 //              until the refinement certifies (k_cyc_*). A near-optimal
 //              flow (config 4's churn rounds) takes the finish a phase earlier.
@@ -2544,23 +2544,20 @@ __global__ void k_pr_apply(DG g, int packed) {
 // 11–13 on config 3, 24–120 arcs of cost −1…−4 each). The refinement's
 // Bellman-Ford (PR = 2) records each node's parent; when it has not converged
 // after a batch of rounds, the parent graph — one parent per node, so its cycles
-// are node-disjoint — is searched: pointer doubling (2^CYC_LOG steps) lands every
-// node of a cycle no longer than that, the least id of each window groups a
-// cycle, one thread per cycle walks it to check its cost (< 0) and bottleneck and
-// pushes the bottleneck around it, and the cycle's nodes rejoin the frontier.
+// are node-disjoint — is searched: pointer doubling (2^k steps) lands every node
+// of a cycle no longer than that, the least id of each window groups a cycle, its
+// nodes sum the cost and take the bottleneck with atomics, a group that is not a
+// union of cycles (nodes disagreeing on the id, a non-residual arc, a node with
+// other than one member pointing at it) is dropped, and every good negative group
+// pushes its bottleneck around in parallel; the cycle's nodes rejoin the frontier.
 // The refinement then continues; once its frontier drains, every residual arc
 // meets d(u) ≤ d(v) + len(u, v): the prices p − d certify the flow optimal.
 constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
 [[maybe_unused]] constexpr int CYC_WALK = 1 << CYC_LOG;
-#ifndef KS_CYC_EVERY
-#define KS_CYC_EVERY 16
-#endif
-constexpr int CYC_EVERY = KS_CYC_EVERY;   // refinement rounds between parent-graph searches
+constexpr int CYC_SHORT = 7;              // a short search's doubling steps
+constexpr int CYC_EVERY = 8;              // refinement rounds between parent-graph searches
 constexpr int CYC_PERIODS = 3;            // rounds + search periods per host check
-#ifndef KS_PRC_UNITS_DIV
-#define KS_PRC_UNITS_DIV 4
-#endif
-constexpr long long kPrcUnitsDiv = KS_PRC_UNITS_DIV;   // an earlier finish (run_phase prc_early)
+constexpr long long kPrcUnitsDiv = 4;   // an earlier finish (run_phase prc_early)
 
 // The parent of every node (itself for a root) from its key's position a (the
 // parent v is the head of a's reverse); its own id as the window minimum; the
@@ -2568,7 +2565,7 @@ constexpr long long kPrcUnitsDiv = KS_PRC_UNITS_DIV;   // an earlier finish (run
 template <bool CP>
 __global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* __restrict__ M,
                           int* __restrict__ onc, int* __restrict__ R, long long* __restrict__ gsum,
-                          long long* __restrict__ gcap, int* __restrict__ gbad) {
+                          long long* __restrict__ gcap, int* __restrict__ gbad, int* __restrict__ indeg) {
     if (g.ctl->bf_done) return;   // the refinement converged: no search
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         const long long a = atom_load(&g.dist[ni(u)]) & PK_NONE;
@@ -2582,6 +2579,7 @@ __global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* 
         gsum[u] = 0;
         gcap[u] = INF64;
         gbad[u] = 0;
+        indeg[u] = 0;
     }
 }
 // one doubling step: 2^k → 2^(k+1) steps ahead, and the least id over them
@@ -2611,15 +2609,16 @@ __global__ void k_cyc_mark(int n, const int* __restrict__ done, const int* __res
 template <bool CP>
 __global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
                             const int* __restrict__ R, long long* __restrict__ gsum, long long* __restrict__ gcap,
-                            int* __restrict__ gbad) {
+                            int* __restrict__ gbad, int* __restrict__ indeg) {
     if (g.ctl->bf_done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         if (!onc[u] || J0[u] == (int)u) continue;
         const int m = MK[u], mn = MK[J0[u]];
-        if (mn != m) {
+        if (mn != m || !onc[J0[u]]) {   // (a parent off every cycle: a chain, not a cycle)
             gbad[m] = 1;
             gbad[mn] = 1;
         }
+        atomicAdd(&indeg[J0[u]], 1);
         const Pos q = PL<CP>::ld_nr(g, R[u]);
         const long long res = q.ucap - q.rcap;   // residual of the reverse: the arc u → v
         if (res <= 0) gbad[m] = 1;
@@ -2627,6 +2626,18 @@ __global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restr
         __hip_atomic_fetch_min(&gcap[m], res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
+// A group is a union of cycles only if each of its nodes has exactly one member
+// pointing at it: a chain longer than the doubling window (its nodes marked too)
+// that runs into a cycle gives the junction two, its first node none, and the
+// group is dropped (pushing along a chain would break conservation).
+__global__ void k_cyc_check(int n, const int* __restrict__ done, const int* __restrict__ J0,
+                            const int* __restrict__ MK, const int* __restrict__ onc, const int* __restrict__ indeg,
+                            int* __restrict__ gbad) {
+    if (*done) return;
+    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK)
+        if (onc[u] && J0[u] != (int)u && atom_load_i(&indeg[u]) != 1) gbad[MK[u]] = 1;
+}
+
 // Cancel every good negative group: each of its nodes pushes the bottleneck along
 // its own parent arc (the arcs of different nodes are different positions), and
 // rejoins the frontier the next refinement round reads (buffer seq).
@@ -2669,7 +2680,7 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
                               const long long* __restrict__ supply, const long long* __restrict__ low,
                               const long long* __restrict__ cap, const long long* __restrict__ cost,
                               long long* __restrict__ flows, long long* __restrict__ part,
-                              long long* __restrict__ partf) {
+                              long long* __restrict__ partf, long long* __restrict__ bal) {
     __shared__ long long sh[WPB];
     long long csum = 0, fsum = 0;
     int bad = 0;
@@ -2690,6 +2701,10 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
         if (rf < 0 || rr < 0 || f < 0 || f != rr) bad = 1;
         const long long fl = f + low[i];
         flows[i] = fl;
+        if (fl) {   // conservation from the flows themselves (k_verify_balance), not from the excess words
+            atom_add(&bal[src[i]], -fl);
+            atom_add(&bal[dst[i]], fl);
+        }
         csum += fl * cost[i];
         if (supply[dst[i]] < 0) fsum += fl;
         if (supply[src[i]] < 0) fsum -= fl;
@@ -2701,6 +2716,17 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
         partf[blockIdx.x] = fsum;
     }
     if (__any(bad) && lane_id() == 0) atomicOr(&g.ctl->verify_bad, 1);
+}
+
+// Every live node's net inflow plus its supply is zero (the sink's supply is the
+// demand set for this solve): conservation of the flow the caller downloads,
+// independent of the solver's own excess bookkeeping.
+__global__ void k_verify_balance(DG g, int ncap, const unsigned char* __restrict__ alive,
+                                 const long long* __restrict__ supply, const long long* __restrict__ bal) {
+    int bad = 0;
+    for (long long v = blockIdx.x * (long long)BLK + threadIdx.x; v < ncap; v += (long long)gridDim.x * BLK)
+        if (alive[v] && atom_load(&bal[v]) + supply[v] != 0) bad = 1;
+    if (__any(bad) && lane_id() == 0) atomicOr(&g.ctl->verify_bad, 4);
 }
 
 __global__ void k_verify_opt(DG g, long long m2) {
@@ -3090,6 +3116,7 @@ struct EngineImpl {
     DBuf<CItem> citems;
     DBuf<int> hnchunks, q_unsat, q_arrive;
     DBuf<long long> q_req, q_taken, q_min, inbox, part, flows;
+    DBuf<long long> vbal;               // verification: per-node balance of the arc flows (input slots)
     DBuf<unsigned char> flags;   // 6 frontier buffers × hub_base
     DBuf<int> hubflags;          // 6 × nheavy
     DBuf<unsigned long long> ctr;
@@ -3178,7 +3205,7 @@ struct EngineImpl {
         capv.release(); capi.release(); rs.release(); sort_tmp.release(); cls.release(); nsel.release();
         for (auto& b : cls_list) b.release();
         sel_tmp.release(); hitems.release(); citems.release(); hnchunks.release(); q_unsat.release(); q_arrive.release();
-        q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release();
+        q_req.release(); q_taken.release(); q_min.release(); inbox.release(); part.release(); flows.release(); vbal.release();
         flags.release(); hubflags.release(); ctr.release(); xl.release(); xl2.release(); bx.release(); fl.release(); fdef.release(); aug_req.release(); ctl.release(); saved_flows.release(); p_slot.release();
         map_outv.release(); map_inv.release(); map_outs.release(); map_ins.release(); map_rank.release();
         map_is_task.release(); flow_sel.release(); flow_cnt.release(); map_itype.release(); map_tmp.release();
@@ -4508,7 +4535,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     unsigned long long gu_prev = 0;   // cycle log: Bellman-Ford relaxations counted so far
     auto prc_refine = [&](int* rounds_used, int cap) -> int {
         KS_CHECK(hipEventRecord(s.ev[6], st));
-        KS_CHECK(s.cyc.ensure((size_t)8 * nn));
+        KS_CHECK(s.cyc.ensure((size_t)9 * nn));
         KS_CHECK(s.cyc64.ensure((size_t)2 * nn));
         int* J0 = s.cyc.p;
         int* Ja = J0 + nn;
@@ -4518,6 +4545,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int* onc = Mb + nn;
         int* R = onc + nn;
         int* gbad = R + nn;
+        int* indeg = gbad + nn;   // members of its group pointing at a node
         long long* gsum = s.cyc64.p;
         long long* gcap = gsum + nn;
         KS_CHECK(set_eps(1));
@@ -4527,17 +4555,23 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
         // their least id, every good negative one cancelled in parallel (each kernel
         // returns at once when the refinement has converged)
+        int nsearch = 0;
         auto search = [&]() {
-            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad);
-            for (int d = 0; d < CYC_LOG; ++d) {
+            // three of four searches double only CYC_SHORT times (cycles of up to 128
+            // arcs: the ones the finish meets); every fourth covers 2^CYC_LOG
+            const int lg = (nsearch++ % 4 == 3) ? CYC_LOG : CYC_SHORT;
+            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad, indeg);
+            for (int d = 0; d < lg; ++d) {
                 if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Jb, Mb, Ja, Ma);
                 else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Ja, Ma, Jb, Mb);
             }
-            const int* JK = (CYC_LOG & 1) ? Jb : Ja;
-            const int* MK = (CYC_LOG & 1) ? Mb : Ma;
+            const int* JK = (lg & 1) ? Jb : Ja;
+            const int* MK = (lg & 1) ? Mb : Ma;
             hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, done, JK, (const int*)J0, onc);
             KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
-                   gbad);
+                   gbad, indeg);
+            hipLaunchKernelGGL(k_cyc_check, dim3(ngrid), dim3(BLK), 0, st, nn, done, (const int*)J0, MK,
+                               (const int*)onc, (const int*)indeg, gbad);
             KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
                    (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
         };
@@ -4818,10 +4852,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (m2) hipLaunchKernelGGL(k_max_viol, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         KS_CHECK(read_ctl());
         const long long viol = s.h_ctl->gu_L;
-#ifndef KS_EXP_WARM_UNITS
-#define KS_EXP_WARM_UNITS 8
-#endif
-        long long e0 = std::max<long long>(1, std::min<long long>({viol, KS_EXP_WARM_UNITS * mult, eps}));
+        constexpr long long kWarmUnits = 8;   // the first warm phase at ≤ 8 cost units
+        long long e0 = std::max<long long>(1, std::min<long long>({viol, kWarmUnits * mult, eps}));
         if (s.cell_layout && (alpha & (alpha - 1)) == 0)   // a power of two ≥ the violation (cell ladder)
             while (e0 & (e0 - 1)) e0 += e0 & -e0;
         warm_thr = e0;
@@ -5016,12 +5048,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         long long sat_thr = phases == 1 && use_warm && !fb
                                 ? warm_thr
                                 : ((pr_failed || fb || (use_warm && o.warm_start >= 2)) ? eps : 0LL);
-#ifdef KS_EXP_SATV
-        {   // EXPERIMENT: phases after the first saturate only the arcs violating their ε
-            const bool lastp = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
-            if (phases > 1 && (KS_EXP_SATV == 2 || lastp)) sat_thr = eps;
-        }
-#endif
         pr_failed = false;
         const bool last_phase = eps / alpha < 1 || eps <= 1 || (use_pr && eps * pr_div < mult);
         // the phase before the final one drains completely when the cycle-cancelling
@@ -5094,12 +5120,18 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipMemsetAsync(&s.ctl.p->verify_bad, 0, sizeof(int), st));
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);
+        KS_CHECK(s.vbal.ensure(std::max<int64_t>(s.ncap, 1)));
+        KS_CHECK(hipMemsetAsync(s.vbal.p, 0, std::max<int64_t>(s.ncap, 1) * sizeof(long long), st));
         if (hi)
             hipLaunchKernelGGL(k_verify_arcs, dim3(vgrid), dim3(BLK), 0, st, g, hi, (const unsigned char*)s.a_alive.p,
                                (const int*)s.fwd.p, (const int*)s.a_src.p, (const int*)s.a_dst.p,
                                (const long long*)s.n_supply.p, (const long long*)s.a_low.p,
                                (const long long*)s.a_cap.p, (const long long*)s.a_cost.p, s.flows.p, s.part.p,
-                               s.part.p + 4096);
+                               s.part.p + 4096, s.vbal.p);
+        if (s.ncap)
+            hipLaunchKernelGGL(k_verify_balance, dim3(grid_for(s.ncap, 2048)), dim3(BLK), 0, st, g, (int)s.ncap,
+                               (const unsigned char*)s.n_alive.p, (const long long*)s.n_supply.p,
+                               (const long long*)s.vbal.p);
         if (m2) hipLaunchKernelGGL(k_verify_opt, dim3(grid_for(m2, 2048)), dim3(BLK), 0, st, g, (long long)m2);
         hipLaunchKernelGGL(k_verify_nodes, dim3(ngrid), dim3(BLK), 0, st, g);
         std::vector<long long> parts(hi ? vgrid : 0), partf(hi ? vgrid : 0);
