@@ -139,7 +139,10 @@ typedef struct ks_opts {
                                   Bit 4 (ks_batch_create*): the middle cell of the
                                   batch gives up in the cell solver (re-solved on the
                                   engine). Bit 5: the cycle-cancelling finish gives
-                                  up after its first batch (the final phase runs).    */
+                                  up after its first batch (the final phase runs).
+                                  Bit 6: one unit is moved on an arc after the solve
+                                  without its endpoints' excess (the verifier's
+                                  conservation check must fail: KS_E_VERIFY).         */
     int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
                                   cycle [1]; later passes retry units left short        */
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —

@@ -2512,6 +2512,21 @@ __global__ void k_fs_end(DG g) {
     if (g.ctl->fs_done && !g.ctl->fs_fail) g.ctl->fs_completed += 1;
 }
 
+// TESTS ONLY (ks_opts.fault_inject bit 6): move one unit on the first arc that can
+// take it without touching any excess word — the flow then violates conservation,
+// which only the verifier's balance of the arc flows can see.
+__global__ void k_break_conservation(DG g, long long m2) {
+    if (threadIdx.x || blockIdx.x) return;
+    for (long long p = 0; p < m2; ++p) {
+        const Pos q = g.pos[p];
+        if (q.rcap > 0 && q.ucap > 0 && q.cost < (1LL << 50)) {
+            g.pos[p].rcap = q.rcap - 1;
+            g.pos[q.rev].rcap += 1;
+            return;
+        }
+    }
+}
+
 // TESTS ONLY (ks_opts.fault_inject bit 1): lower one node's price by delta after
 // the solve, so the certificate fails on an optimal flow and must be repaired.
 __global__ void k_perturb_price(DG g, int x, long long delta) {
@@ -5117,6 +5132,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                                (const CPos*)s.cpos.p, s.pos.p);
             cp_dirty = false;
         }
+        if ((o.fault_inject & 64) && m2)   // TESTS ONLY: break conservation, not the excess words
+            hipLaunchKernelGGL(k_break_conservation, dim3(1), dim3(64), 0, st, g, (long long)m2);
         KS_CHECK(hipMemsetAsync(&s.ctl.p->verify_bad, 0, sizeof(int), st));
         KS_CHECK(set_eps(1));
         hipLaunchKernelGGL(k_drain_all, dim3((std::max(1, s.nheavy) + BLK - 1) / BLK), dim3(BLK), 0, st, g);

@@ -377,6 +377,22 @@ def test_failed_load_leaves_the_context_usable(ctx):
     check_mapping(g, ctx.task_mapping())
 
 
+@pytest.mark.parametrize("path", ["engine", "cell"])
+def test_verifier_checks_conservation_from_the_flows(path):
+    """The verifier balances every node from the arc flows the caller downloads
+    (plus its supply), not from the solver's excess words: fault_inject bit 6
+    moves one unit on an arc after the solve without touching any excess, and the
+    solve must fail with KS_E_VERIFY (conservation) instead of returning a flow
+    that breaks it (north star: conservation verified on every solve)."""
+    g = gen.quincy(2_000, 200, 5, 20, 4)
+    with native.Context(0, cell_nodes=20_000 if path == "cell" else -1, fault_inject=64) as c:
+        c.load_graph(g)
+        with pytest.raises(native.KsError) as e:
+            c.solve()
+        assert e.value.code == native.KS_E_VERIFY
+        assert "conservation" in str(e.value)
+
+
 def test_cell_range_fallback_on_a_warm_start():
     """a warm solve whose new costs no longer fit the cell solver's
     compact record (scaled cost · (n+1) beyond int32) falls back to the engine; the
