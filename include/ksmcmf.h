@@ -64,12 +64,16 @@
 extern "C" {
 #endif
 
-#define KSMCMF_ABI_VERSION 4   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls;
+#define KSMCMF_ABI_VERSION 5   /* 2: ks_opts tuning fields, ks_result.recoveries, batch layout calls;
                                   3: ks_opts.cell_nodes, ks_result per-kind timing and cell-solver
-                                  fields; 4: ks_opts.compact_pos (the last reserved word),
-                                  ks_result.cell_fallbacks (a reserved word), sizes unchanged.
-                                  ks_opts (96 B) and ks_result (320 B) CHANGED SIZE in
-                                  ABI 2 and ks_result again in ABI 3: a caller must check
+                                  fields; 4: ks_opts.compact_pos (the last reserved word of
+                                  ks_opts), and three words of ks_result repurposed:
+                                  cell_fallbacks and cycles_cancelled (two reserved words)
+                                  and compact (the former _pad3); 5: ks_result.fb_resets
+                                  (the last reserved word) and ks_result.cycles_rejected;
+                                  ks_result grew to 352 B (3 reserved words).
+                                  ks_opts (96 B) CHANGED SIZE in ABI 2 and ks_result in
+                                  ABI 2, 3 and 5: a caller must check
                                   ks_abi_version() == KSMCMF_ABI_VERSION before ks_create. */
 
 /* status codes (0 = OK) */
@@ -137,12 +141,23 @@ typedef struct ks_opts {
                                   (ks_batch_create*): rank 0's receive buffer
                                   allocation fails in ks_batch_gather (the same).
                                   Bit 4 (ks_batch_create*): the middle cell of the
-                                  batch gives up in the cell solver (re-solved on the
-                                  engine). Bit 5: the cycle-cancelling finish gives
+                                  batch gives up in the cell solver and is re-solved
+                                  on the engine; the result then reports solver 1,
+                                  cells = the batch's cells, warm_started 1 (the
+                                  other cells' optima are carried), cell_fallbacks 1
+                                  and fb_resets. Bit 5: the cycle-cancelling finish gives
                                   up after its first batch (the final phase runs).
                                   Bit 6: one unit is moved on an arc after the solve
                                   without its endpoints' excess (the verifier's
-                                  conservation check must fail: KS_E_VERIFY).         */
+                                  conservation check must fail: KS_E_VERIFY).
+                                  Bit 7: every parent-graph search of the finish
+                                  doubles only 5 steps (a 32-node window, shorter than
+                                  the parent chains: their nodes are marked and meet
+                                  cycles, and the union-of-cycles test must reject
+                                  them — cycles_rejected). Bit 8 (engine): that test
+                                  only counts, rejecting nothing (with bit 7 a chain
+                                  is pushed along: the verifier must then fail the
+                                  solve with KS_E_VERIFY, never return a wrong cost). */
     int32_t  walk_passes;      /* tail walker passes from the update's excess nodes per
                                   cycle [1]; later passes retry units left short        */
     int32_t  tail_nodes;       /* a phase's tail — walks over each update, few sweeps —
@@ -264,7 +279,14 @@ typedef struct ks_result {
                                   kept (the status stays KS_OK)                         */
     uint64_t cycles_cancelled; /* negative cycles the cycle-cancelling finish cancelled
                                   (ks_opts.price_refine 1)                  */
-    uint64_t reserved2[1];
+    uint64_t fb_resets;        /* ABI 5. A per-cell fallback solve: live arc slots plus
+                                  node slots of the failing cells whose carried flow /
+                                  price it reset (they restart cold; 0 otherwise)      */
+    uint64_t cycles_rejected;  /* ABI 5. The finish's parent-graph searches: marked nodes
+                                  the union-of-cycles test found with other than one
+                                  member pointing at them (engine), or leader walks
+                                  that did not close a cycle (cell solver)            */
+    uint64_t reserved3[3];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

@@ -40,14 +40,16 @@ def _flags(arch: str, defines=()) -> list[str]:
             "-I" + os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
 
 
-def _compile_all(arch: str, tag: str, defines=(), force: bool = False, verbose: bool = False) -> list[str]:
+def _compile_all(arch: str, tag: str, defines=(), force: bool = False, verbose: bool = False,
+                 extra=()) -> list[str]:
     """One object per source, compiled in parallel (a source is rebuilt when it or
     any header is newer than its object)."""
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OBJ_DIR, exist_ok=True)
     hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    sources = list(SOURCES) + list(extra)
     jobs = []
-    for src in SOURCES:
+    for src in sources:
         obj = os.path.join(OBJ_DIR, f"{tag}_{os.path.basename(src)}.o")
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
             jobs.append((src, obj))
@@ -60,7 +62,7 @@ def _compile_all(arch: str, tag: str, defines=(), force: bool = False, verbose: 
         os.replace(obj + ".tmp", obj)
     with ThreadPoolExecutor(max(1, min(len(jobs), os.cpu_count() or 1))) as ex:
         list(ex.map(run, jobs))
-    return [os.path.join(OBJ_DIR, f"{tag}_{os.path.basename(src)}.o") for src in SOURCES]
+    return [os.path.join(OBJ_DIR, f"{tag}_{os.path.basename(src)}.o") for src in sources]
 
 
 def _link(objs: list[str], arch: str, out: str, verbose: bool = False):
@@ -95,7 +97,28 @@ def build_daemon(force: bool = False) -> str:
     return DAEMON
 
 
+FAKE_COMM_SRC = os.path.join(ROOT, "tests", "fake_comm", "fake_nccl.cpp")
+FAKE_COMM_TAG = "fakecomm"
+
+
+def build_fake_comm(force: bool = False) -> str:
+    """TEST INFRASTRUCTURE: libksmcmf_fakecomm.so, the library compiled with
+    -DKS_FAKE_COMM and tests/fake_comm/fake_nccl.cpp (RCCL's entry points for the
+    ranks of one process) for the world-2 rehearsal of ks_batch_gather on one GPU.
+    The shipped libksmcmf.so is built without either."""
+    out = variant_path(FAKE_COMM_TAG)
+    deps = DEPS + [FAKE_COMM_SRC]
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(p) for p in deps):
+        return out
+    arch = os.environ.get("KS_OFFLOAD_ARCH", "gfx950")
+    _link(_compile_all(arch, "v_" + FAKE_COMM_TAG, ["KS_FAKE_COMM"], force=force, extra=[FAKE_COMM_SRC]), arch, out)
+    return out
+
+
 def variant_path(tag: str) -> str:
+    """ksched_amd/libksmcmf_<tag>.so; tags are plain identifiers (no paths)."""
+    if not tag.replace("_", "").isalnum():
+        raise ValueError(f"library variant tag {tag!r}: letters, digits and _ only")
     return os.path.join(HERE, f"libksmcmf_{tag}.so")
 
 
@@ -109,3 +132,4 @@ def build_variant(tag: str, defines: list[str]) -> str:
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_daemon(force=True))
+    print(build_fake_comm(force=True))

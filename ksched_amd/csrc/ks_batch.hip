@@ -15,6 +15,11 @@
 // under torch.distributed.run: ncclCommInitRank with an id from rank 0).
 // RCCL is loaded with dlopen on the first batch (the single-graph API never
 // needs it); a process that already holds RCCL (torch) shares its copy.
+// A TEST build of the library (-DKS_FAKE_COMM: libksmcmf_fakecomm.so, made by
+// ksched_amd/_build.py build_fake_comm, never the shipped libksmcmf.so) binds the
+// same entry points to tests/fake_comm/fake_nccl.cpp compiled into it instead —
+// the ranks of one process on one GPU — so the world > 1 path of ks_batch_gather
+// runs on a one-GPU box.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -24,6 +29,21 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#ifdef KS_FAKE_COMM
+extern "C" {
+ncclResult_t ks_fake_ncclGetUniqueId(ncclUniqueId*);
+ncclResult_t ks_fake_ncclCommInitAll(ncclComm_t*, int, const int*);
+ncclResult_t ks_fake_ncclCommInitRank(ncclComm_t*, int, ncclUniqueId, int);
+ncclResult_t ks_fake_ncclCommDestroy(ncclComm_t);
+ncclResult_t ks_fake_ncclGroupStart();
+ncclResult_t ks_fake_ncclGroupEnd();
+ncclResult_t ks_fake_ncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+ncclResult_t ks_fake_ncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+ncclResult_t ks_fake_ncclAllReduce(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+const char* ks_fake_ncclGetErrorString(ncclResult_t);
+}
+#endif
 
 #include "ks_ctx.h"
 
@@ -45,6 +65,21 @@ struct Rccl {
 
     bool load(std::string& err) {
         if (h) return true;
+#ifdef KS_FAKE_COMM
+        GetUniqueId = ks_fake_ncclGetUniqueId;
+        CommInitAll = ks_fake_ncclCommInitAll;
+        CommInitRank = ks_fake_ncclCommInitRank;
+        CommDestroy = ks_fake_ncclCommDestroy;
+        GroupStart = ks_fake_ncclGroupStart;
+        GroupEnd = ks_fake_ncclGroupEnd;
+        Send = ks_fake_ncclSend;
+        Recv = ks_fake_ncclRecv;
+        AllReduce = ks_fake_ncclAllReduce;
+        GetErrorString = ks_fake_ncclGetErrorString;
+        h = this;
+        (void)err;
+        return true;
+#endif
         for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
             h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
             if (h) break;
@@ -73,9 +108,10 @@ struct Rccl {
     }
 };
 
-Rccl& rccl() {
+// RCCL, loaded on first use (the test build: the fake in-process ranks)
+Rccl* comm_lib(std::string& err) {
     static Rccl r;
-    return r;
+    return r.load(err) ? &r : nullptr;
 }
 
 // ---- row layout of ks_batch_gather (host code, shared by the packing, the
@@ -118,6 +154,7 @@ struct ks_batch {
         ks_result res{};
     };
     std::vector<Local> loc;
+    const Rccl* nccl = nullptr;         // the communication library behind this batch
     int world = 1;
     size_t ngraphs = 0;
     std::string err;
@@ -140,9 +177,10 @@ namespace {
         if (_e != hipSuccess) return b->fail(KS_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
-ks_batch* make_batch(int world, const ks_opts* opts, const std::vector<std::pair<int, int>>& dev_rank) {
+ks_batch* make_batch(const Rccl* api, int world, const ks_opts* opts, const std::vector<std::pair<int, int>>& dev_rank) {
     ks_batch* b = new (std::nothrow) ks_batch;
     if (!b) return nullptr;
+    b->nccl = api;
     b->world = world;
     b->fault_pack = (opts && (opts->fault_inject & 4)) ? 1 : 0;   // TESTS ONLY: global rank 0's packing fails
     b->fault_root = (opts && (opts->fault_inject & 8)) ? 1 : 0;   // TESTS ONLY: rank 0's root buffer allocation fails
@@ -204,22 +242,24 @@ int ks_batch_unpack(const int64_t* gathered, size_t ngraphs, int world, size_t m
 
 int ks_batch_unique_id(uint8_t* id) {
     std::string err;
-    if (!id || !rccl().load(err)) return KS_E_DEVICE;
+    const Rccl* api = id ? comm_lib(err) : nullptr;
+    if (!api) return KS_E_DEVICE;
     ncclUniqueId u;
-    if (rccl().GetUniqueId(&u) != ncclSuccess) return KS_E_DEVICE;
+    if (api->GetUniqueId(&u) != ncclSuccess) return KS_E_DEVICE;
     std::memcpy(id, u.internal, KS_UNIQUE_ID_BYTES);
     return KS_OK;
 }
 
 ks_batch* ks_batch_create(const int* devices, int ndev, const ks_opts* opts) {
     std::string err;
-    if (!devices || ndev < 1 || !rccl().load(err)) return nullptr;
+    const Rccl* api = devices && ndev >= 1 ? comm_lib(err) : nullptr;
+    if (!api) return nullptr;
     std::vector<std::pair<int, int>> dr;
     for (int i = 0; i < ndev; ++i) dr.emplace_back(devices[i], i);
-    ks_batch* b = make_batch(ndev, opts, dr);
+    ks_batch* b = make_batch(api, ndev, opts, dr);
     if (!b) return nullptr;
     std::vector<ncclComm_t> comms(ndev);
-    if (rccl().CommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
+    if (api->CommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
         ks_batch_destroy(b);
         return nullptr;
     }
@@ -229,12 +269,13 @@ ks_batch* ks_batch_create(const int* devices, int ndev, const ks_opts* opts) {
 
 ks_batch* ks_batch_create_rank(int device, int nranks, int rank, const uint8_t* id, const ks_opts* opts) {
     std::string err;
-    if (!id || nranks < 1 || rank < 0 || rank >= nranks || !rccl().load(err)) return nullptr;
-    ks_batch* b = make_batch(nranks, opts, {{device, rank}});
+    const Rccl* api = id && nranks >= 1 && rank >= 0 && rank < nranks ? comm_lib(err) : nullptr;
+    if (!api) return nullptr;
+    ks_batch* b = make_batch(api, nranks, opts, {{device, rank}});
     if (!b) return nullptr;
     ncclUniqueId u;
     std::memcpy(u.internal, id, KS_UNIQUE_ID_BYTES);
-    if (hipSetDevice(device) != hipSuccess || rccl().CommInitRank(&b->loc[0].comm, nranks, u, rank) != ncclSuccess) {
+    if (hipSetDevice(device) != hipSuccess || api->CommInitRank(&b->loc[0].comm, nranks, u, rank) != ncclSuccess) {
         ks_batch_destroy(b);
         return nullptr;
     }
@@ -245,7 +286,7 @@ void ks_batch_destroy(ks_batch* b) {
     if (!b) return;
     for (auto& l : b->loc) {
         (void)hipSetDevice(l.device);
-        if (l.comm) rccl().CommDestroy(l.comm);
+        if (l.comm) b->nccl->CommDestroy(l.comm);
         if (l.rows) (void)hipFree(l.rows);
         if (l.scratch) (void)hipFree(l.scratch);
         if (l.stat) (void)hipFree(l.stat);
@@ -460,14 +501,14 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
             }
         }
         {   // (the group is always closed: an RCCL error is returned after GroupEnd)
-            ncclResult_t nr = rccl().GroupStart();
+            ncclResult_t nr = b->nccl->GroupStart();
             for (auto& l : b->loc) {
-                const ncclResult_t x = rccl().AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream());
+                const ncclResult_t x = b->nccl->AllReduce(l.stat, l.stat, 1, ncclInt64, ncclMin, l.comm, l.ctx->eng.stream());
                 if (nr == ncclSuccess) nr = x;
             }
-            const ncclResult_t ge = rccl().GroupEnd();
+            const ncclResult_t ge = b->nccl->GroupEnd();
             if (nr == ncclSuccess) nr = ge;
-            if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("status all-reduce: ") + rccl().GetErrorString(nr));
+            if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("status all-reduce: ") + b->nccl->GetErrorString(nr));
         }
         long long worst = 0;
         for (size_t li = 0; li < b->loc.size(); ++li) {
@@ -491,22 +532,22 @@ int ks_batch_gather(ks_batch* b, size_t max_tasks, uint64_t* pu, int64_t* cost, 
     //    returned after the group, so no peer is left waiting in a send.
     long long* rbuf = root_loc >= 0 ? b->root_buf : nullptr;
     if (b->world > 1) {
-        ncclResult_t nr = rccl().GroupStart();
+        ncclResult_t nr = b->nccl->GroupStart();
         for (auto& l : b->loc) {
             hipStream_t st = l.ctx->eng.stream();
             if (l.grank == 0) {
                 for (int r = 1; r < b->world; ++r) {
-                    const ncclResult_t x = rccl().Recv(rbuf + (size_t)r * block, block, ncclInt64, r, l.comm, st);
+                    const ncclResult_t x = b->nccl->Recv(rbuf + (size_t)r * block, block, ncclInt64, r, l.comm, st);
                     if (nr == ncclSuccess) nr = x;
                 }
             } else {
-                const ncclResult_t x = rccl().Send(l.rows, block, ncclInt64, 0, l.comm, st);
+                const ncclResult_t x = b->nccl->Send(l.rows, block, ncclInt64, 0, l.comm, st);
                 if (nr == ncclSuccess) nr = x;
             }
         }
-        const ncclResult_t ge = rccl().GroupEnd();
+        const ncclResult_t ge = b->nccl->GroupEnd();
         if (nr == ncclSuccess) nr = ge;
-        if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("ncclSend/ncclRecv group: ") + rccl().GetErrorString(nr));
+        if (nr != ncclSuccess) return b->fail(KS_E_DEVICE, std::string("ncclSend/ncclRecv group: ") + b->nccl->GetErrorString(nr));
     }
     for (auto& l : b->loc) {
         KB_HIP(hipSetDevice(l.device));

@@ -70,6 +70,7 @@ struct CellOut {
     int last_eps;          // 1 when the solve ended at ε = 1 (scaled)
     int cycles;            // negative cycles the cycle-cancelling finish cancelled
     int searches;          // its parent-graph searches
+    int rejected;          // leaders whose walk did not close a cycle (a chain, a longer cycle)
     unsigned cyc_dbg[4];   // diagnostics: nodes with a parent, marked on a cycle, leaders, closed walks
     unsigned long long sweeps, bf_rounds, scans, visits, pushes, relabels, gu_scans;
     unsigned long long ticks;   // s_memrealtime ticks (100 MHz) of the cell's solve
@@ -123,6 +124,7 @@ struct CellArgs {
     const int* bad;          // set by k_cell_pack: a value the compact record cannot hold
     int fault_cell;          // TESTS ONLY (ks_opts.fault_inject bit 4): this cell stops after
     int fault_ops;           //   fault_ops operations with CS_NOCONV (−1: none)
+    int cyc_lg;              // the finish's doubling steps (CYC_LOG; TESTS ONLY, fault_inject bit 7: 5)
 };
 
 // LDS one workgroup needs for cells of up to n nodes (0 when they do not fit in
@@ -132,6 +134,8 @@ size_t cell_lds_bytes(int n, size_t limit);
 int cell_max_nodes(size_t limit);
 // k_cell_pack → k_cell → k_cell_unpack on st; *bad (device int) is set when a
 // position does not fit the compact record (every cell then returns CS_RANGE).
-hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st);
+// *refused: the device will not run k_cell at this size (its LDS); any other
+// error is a real launch failure
+hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st, bool* refused);
 
 }  // namespace ks

@@ -1082,6 +1082,7 @@ struct Ctl {
     int drain;                // this phase drains: the cycle-cancelling finish follows it
     int prc, prc_tried;       // the finish's refinement is running / was tried
     int cycles, searches;     // cycles it cancelled, parent-graph searches
+    int rejected;             // leader walks that did not close a cycle
     unsigned cyc_dbg[4];
     unsigned long long phase_sweeps, sweeps, rounds;
     unsigned long long t_op;                // when the running operation started
@@ -1398,7 +1399,8 @@ __device__ __forceinline__ void cyc_search(const CellArgs& A, const K& k, int sr
         dbg[0] += a >= 0;
     }
     __syncthreads();
-    for (int d = 0; d < CYC_LOG; ++d) {
+    const int lg = A.cyc_lg;   // CYC_LOG (a shorter window only under fault_inject bit 7)
+    for (int d = 0; d < lg; ++d) {
         const int* Wi = Wb[d & 1];
         int* Wo = Wb[(d & 1) ^ 1];
         for (int l = threadIdx.x; l < k.N; l += CT) {
@@ -1408,13 +1410,16 @@ __device__ __forceinline__ void cyc_search(const CellArgs& A, const K& k, int sr
         }
         __syncthreads();
     }
-    W = Wb[CYC_LOG & 1];
+    W = Wb[lg & 1];
     for (int l = threadIdx.x; l < k.N; l += CT) {
         const int x = W[l] & CYC_IDM;
         if (key_at(key, x) >= 0 && !(atomicOr(&W[x], CYC_ON) & CYC_ON)) ++dbg[1];
     }
     __syncthreads();
-    int found = 0;
+    // A leader's walk is the whole check: a marked node whose window minimum is itself
+    // but which lies on a chain (longer than the window) walks up into a cycle and never
+    // returns to itself, so nothing is pushed (counted in rejected)
+    int found = 0, rejected = 0;
     for (int l = threadIdx.x; l < k.N; l += CT) {
         const int w = W[l];
         if (!(w & CYC_ON) || ((w & ~CYC_ON) >> CYC_IDB) != l) continue;
@@ -1437,6 +1442,7 @@ __device__ __forceinline__ void cyc_search(const CellArgs& A, const K& k, int sr
             }
         }
         dbg[3] += ok;
+        rejected += !ok;
         if (!ok || cost >= 0) continue;
         x = l;
         do {
@@ -1450,6 +1456,7 @@ __device__ __forceinline__ void cyc_search(const CellArgs& A, const K& k, int sr
         ++found;
     }
     if (found) atomicAdd(&c_.cycles, found);
+    if (rejected) atomicAdd(&c_.rejected, rejected);
     for (int i = 0; i < 4; ++i)
         if (dbg[i]) atomicAdd(&c_.cyc_dbg[i], dbg[i]);
 }
@@ -1616,6 +1623,7 @@ __global__ __launch_bounds__(CT) void k_cell(CellArgs A) {
         o.last_eps = c.ended_at_one;
         o.cycles = c.cycles;
         o.searches = c.searches;
+        o.rejected = c.rejected;
         for (int i = 0; i < 4; ++i) o.cyc_dbg[i] = c.cyc_dbg[i];
         o.sweeps = c.sweeps;
         o.bf_rounds = c.rounds;
@@ -1703,13 +1711,20 @@ int cell_max_nodes(size_t limit) {
     return lo;
 }
 
-hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st) {
+hipError_t cell_launch(const CellArgs& a, int* bad, size_t lds_limit, hipStream_t st, bool* refused) {
+    *refused = false;
     const size_t lds = cell_lds_bytes(a.max_nodes, lds_limit);
-    if (!lds || a.ncells <= 0) return hipErrorInvalidValue;
+    if (!lds || a.ncells <= 0) {
+        *refused = true;
+        return hipErrorInvalidValue;
+    }
     // (per device and cheap: set on every launch)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cell),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+        *refused = e == hipErrorInvalidValue;   // the device will not give k_cell that much LDS
+        return e;
+    }
     if ((e = hipMemsetAsync(bad, 0, sizeof(int), st)) != hipSuccess) return e;
     const int pg = (int)std::min<long long>(4096, (a.m2 + 255) / 256 > 0 ? (a.m2 + 255) / 256 : 1);
     hipLaunchKernelGGL(k_cell_pack, dim3(pg), dim3(256), 0, st, a, bad);

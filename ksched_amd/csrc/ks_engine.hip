@@ -124,6 +124,7 @@ struct Ctl {
     int verify_bad;
     int cp_bad;            // k_pack_pos: a value the 16-B record cannot hold (the solve reads Pos)
     int cyc_done;          // cycle-cancelling refinement: cycles cancelled
+    int cyc_rej;           //   marked nodes k_cyc_check found with other than one member pointing at them
     int bf_count;          // Bellman-Ford rounds that did work (whole solve)
     int bfa[3];            // Bellman-Ford flag buffer k holds at least one flag
     int apply_act;         // the global-update apply seeded a non-empty frontier
@@ -2645,12 +2646,20 @@ __global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restr
 // pointing at it: a chain longer than the doubling window (its nodes marked too)
 // that runs into a cycle gives the junction two, its first node none, and the
 // group is dropped (pushing along a chain would break conservation).
+// Such nodes are counted (ctl->cyc_rej); apply = 0 (TESTS ONLY, fault_inject bit 8)
+// counts them without dropping their groups.
 __global__ void k_cyc_check(int n, const int* __restrict__ done, const int* __restrict__ J0,
                             const int* __restrict__ MK, const int* __restrict__ onc, const int* __restrict__ indeg,
-                            int* __restrict__ gbad) {
+                            int* __restrict__ gbad, int apply, int* __restrict__ rej) {
     if (*done) return;
+    int cnt = 0;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK)
-        if (onc[u] && J0[u] != (int)u && atom_load_i(&indeg[u]) != 1) gbad[MK[u]] = 1;
+        if (onc[u] && J0[u] != (int)u && atom_load_i(&indeg[u]) != 1) {
+            if (apply) gbad[MK[u]] = 1;
+            ++cnt;
+        }
+    cnt = (int)wave_sum(cnt);
+    if (cnt && lane_id() == 0) atomicAdd(rej, cnt);
 }
 
 // Cancel every good negative group: each of its nodes pushes the bottleneck along
@@ -2678,6 +2687,152 @@ __global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int* __restri
     if (__any(out) && lane_id() == 0) g.ctl->bfa[seq % 3] = 1;
     cyc = (int)wave_sum(cyc);
     if (cyc && lane_id() == 0) atomicAdd(&g.ctl->cyc_done, cyc);
+}
+
+// The whole search in ONE workgroup with the parent graph in LDS (graphs of at most
+// CYC_LDS_K · 1024 internal ids that the LDS holds: config 2's cells). Round 5
+// measured a one-workgroup search over global memory slower than the 12 launches;
+// here every doubling step, the marks and the in-degrees stay in LDS — three words
+// per node: the parent (J0) and the doubling words (jump | least id << CYC_LDS_IDB,
+// double-buffered as in the cell solver; the free buffer holds the in-degrees
+// afterwards). Each thread owns CYC_LDS_K nodes and issues their loads together
+// (the parents' keys, then the reverse positions, then the heads: three dependent
+// levels in all, not three per node). Only the marked nodes touch global memory
+// after that: their group sums (zeroed by the group's own members) and the pushes.
+// Same steps and the same union-of-cycles test as k_cyc_par … k_cyc_push.
+constexpr int CYC_LDS_T = 1024;
+constexpr int CYC_LDS_K = 14;              // nodes per thread
+constexpr int CYC_LDS_IDB = 15;
+constexpr int CYC_LDS_IDM = (1 << CYC_LDS_IDB) - 1;
+constexpr int CYC_LDS_ON = 1 << 30;
+constexpr int CYC_LDS_MAX = CYC_LDS_K * CYC_LDS_T;   // (< 2^15: ids fit the packed word)
+static_assert(CYC_LDS_MAX <= CYC_LDS_IDM, "node ids must fit the packed doubling word");
+__host__ __device__ constexpr size_t cyc_lds_bytes(int n) { return (size_t)3 * sizeof(int) * (size_t)n; }
+
+template <bool CP>
+__global__ __launch_bounds__(CYC_LDS_T) void k_cyc_lds(DG g, int lg, int apply_check, int seq,
+                                                      long long* __restrict__ gsum, long long* __restrict__ gcap,
+                                                      int* __restrict__ gbad) {
+    if (g.ctl->bf_done) return;   // the refinement converged: no search
+    extern __shared__ int cyc_sm[];
+    const int n = g.n;
+    int* J0 = cyc_sm;
+    int* Wi = cyc_sm + n;
+    int* Wo = Wi + n;
+    const int t = threadIdx.x;
+    {   // parents: each level's loads for all of this thread's nodes issued together
+        long long key[CYC_LDS_K];
+        int rv[CYC_LDS_K], hd[CYC_LDS_K];
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) {
+            const int u = t + k * CYC_LDS_T;
+            key[k] = u < n ? atom_load(&g.dist[ni(u)]) & PK_NONE : PK_NONE;
+        }
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) rv[k] = PL<CP>::rev(g, key[k] != PK_NONE ? (int)key[k] : 0);
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) hd[k] = PL<CP>::head(g, rv[k]);
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) {
+            const int u = t + k * CYC_LDS_T;
+            if (u < n) {
+                const int v = key[k] != PK_NONE ? hd[k] : u;
+                J0[u] = v;
+                Wi[u] = v | (u << CYC_LDS_IDB);
+            }
+        }
+    }
+    __syncthreads();
+    for (int d = 0; d < lg; ++d) {   // 2^d steps ahead, then 2^d more; the least id over them
+        int w[CYC_LDS_K], wx[CYC_LDS_K];
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) {
+            const int u = t + k * CYC_LDS_T;
+            w[k] = u < n ? Wi[u] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) wx[k] = Wi[w[k] & CYC_LDS_IDM];
+#pragma unroll
+        for (int k = 0; k < CYC_LDS_K; ++k) {
+            const int u = t + k * CYC_LDS_T;
+            if (u < n)
+                Wo[u] = (wx[k] & CYC_LDS_IDM) | (min(w[k] >> CYC_LDS_IDB, wx[k] >> CYC_LDS_IDB) << CYC_LDS_IDB);
+        }
+        __syncthreads();
+        int* tmp = Wi;
+        Wi = Wo;
+        Wo = tmp;
+    }
+    // every node a window ahead of another lies on a cycle (or, past the window, on
+    // a chain — the test below); roots are skipped. Wo now holds the in-degrees.
+    for (int u = t; u < n; u += CYC_LDS_T) {
+        const int x = Wi[u] & CYC_LDS_IDM;
+        if (J0[x] != x) atomicOr(&Wi[x], CYC_LDS_ON);
+        Wo[u] = 0;
+    }
+    __syncthreads();
+    // the marked nodes reset their group's sums (every member writes the same values)
+    for (int u = t; u < n; u += CYC_LDS_T) {
+        const int w = Wi[u];
+        if (!(w & CYC_LDS_ON) || J0[u] == u) continue;
+        const int m = (w & ~CYC_LDS_ON) >> CYC_LDS_IDB;
+        gsum[m] = 0;
+        gcap[m] = INF64;
+        gbad[m] = 0;
+    }
+    __syncthreads();
+    for (int u = t; u < n; u += CYC_LDS_T) {
+        const int w = Wi[u];
+        const int p = J0[u];
+        if (!(w & CYC_LDS_ON) || p == u) continue;
+        const int m = (w & ~CYC_LDS_ON) >> CYC_LDS_IDB;
+        const int wp = Wi[p];
+        const int mn = (wp & ~CYC_LDS_ON) >> CYC_LDS_IDB;
+        if (mn != m || !(wp & CYC_LDS_ON)) {   // (a parent off every cycle: a chain, not a cycle)
+            gbad[m] = 1;
+            gbad[mn] = 1;
+        }
+        atomicAdd(&Wo[p], 1);
+        const int a = (int)(atom_load(&g.dist[ni(u)]) & PK_NONE);
+        const Pos q = PL<CP>::ld_nr(g, a);
+        const long long res = q.ucap - q.rcap;   // residual of the reverse: the arc u → v
+        if (res <= 0) gbad[m] = 1;
+        __hip_atomic_fetch_add(&gsum[m], -q.cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_min(&gcap[m], res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    int rej = 0;
+    for (int u = t; u < n; u += CYC_LDS_T) {   // the union-of-cycles test (k_cyc_check)
+        const int w = Wi[u];
+        if ((w & CYC_LDS_ON) && J0[u] != u && Wo[u] != 1) {
+            if (apply_check) gbad[(w & ~CYC_LDS_ON) >> CYC_LDS_IDB] = 1;
+            ++rej;
+        }
+    }
+    __syncthreads();
+    const Front F = g.bf[seq % 3];
+    int out = 0, cyc = 0;
+    for (int u = t; u < n; u += CYC_LDS_T) {
+        const int w = Wi[u];
+        if (!(w & CYC_LDS_ON) || J0[u] == u) continue;
+        const int m = (w & ~CYC_LDS_ON) >> CYC_LDS_IDB;
+        // (agent-scope loads: the sums were made by atomics in L2, never from a stale L1 line)
+        const long long dl = atom_load(&gcap[m]);
+        if (atom_load_i(&gbad[m]) || atom_load(&gsum[m]) >= 0 || dl <= 0 || dl >= INF64) continue;
+        const int a = (int)(atom_load(&g.dist[ni(u)]) & PK_NONE);
+        const Pos q = PL<CP>::ld(g, a);
+        PL<CP>::set_rc(g, a, q.rcap + dl);        // the arc u → v is rev(a): its residual falls by dl
+        PL<CP>::add_rc(g, q.rev, -dl);
+        mark(g, F, u, out);
+        cyc += u == m;
+    }
+    if (__any(out) && lane_id() == 0) g.ctl->bfa[seq % 3] = 1;
+    cyc = (int)wave_sum(cyc);
+    rej = (int)wave_sum(rej);
+    if (lane_id() == 0) {
+        if (cyc) atomicAdd(&g.ctl->cyc_done, cyc);
+        if (rej) atomicAdd(&g.ctl->cyc_rej, rej);
+    }
 }
 
 // ================================================================ verify ===
@@ -2800,9 +2955,12 @@ __global__ void k_restore_flows(int hi, const unsigned char* __restrict__ alive,
 // Per-cell fallback: the cells in rng (node-slot ranges [lo, hi),
 // nr of them) restart cold on the multi-kernel engine — their arcs' carried flows
 // and their nodes' carried prices are zeroed between the save and the restore.
+// *resets counts the live arc slots and node slots it reset (ks_result.fb_resets).
 __global__ void k_fb_reset(int hi, int ncap, int nr, const long long* __restrict__ rng, const int* __restrict__ a_src,
-                           long long* __restrict__ saved, long long* __restrict__ pslot) {
+                           const unsigned char* __restrict__ alive, long long* __restrict__ saved,
+                           long long* __restrict__ pslot, unsigned long long* __restrict__ resets) {
     const long long n = hi > ncap ? hi : ncap;
+    unsigned long long cnt = 0;
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < n; i += (long long)gridDim.x * BLK) {
         const long long vs = i < hi ? a_src[i] : -1, vn = i < ncap ? i : -1;
         bool rs = false, rn = false;
@@ -2812,7 +2970,10 @@ __global__ void k_fb_reset(int hi, int ncap, int nr, const long long* __restrict
         }
         if (rs) saved[i] = 0;
         if (rn) pslot[i] = 0;
+        cnt += (rs && alive[i] ? 1 : 0) + (rn ? 1 : 0);
     }
+    cnt = (unsigned long long)wave_sum((long long)cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(resets, cnt);
 }
 
 __global__ void k_save_prices(int ncap, const int* __restrict__ perm, const long long* __restrict__ p0,
@@ -3172,6 +3333,7 @@ struct EngineImpl {
     bool fb_active = false;             // a per-cell fallback solve is running (engine order, failing cells cold)
     std::vector<int> fb_cells;          // the cells it re-solves
     DBuf<long long> fb_rng;             // their node-slot ranges on the device
+    DBuf<unsigned long long> fb_cnt;    // arc + node slots k_fb_reset restarted cold
     std::vector<CellOut> h_cell_out;
     // ---- scheduler-side sweeps (ks_sched.hip)
     DBuf<int> sched_i;                  // int scratch
@@ -4289,6 +4451,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.recoveries = 0;
     res.cell_fallbacks = 0;
     res.cycles_cancelled = 0;
+    res.fb_resets = 0;
+    res.cycles_rejected = 0;
     KS_CHECK(hipEventRecord(s.ev[0], st));
     KS_CHECK(hipMemsetAsync(s.ctr.p, 0, CTR_SHARDS * NCTR * sizeof(unsigned long long), st));
     KS_CHECK(hipMemsetAsync(s.ctl.p, 0, sizeof(Ctl), st));
@@ -4323,10 +4487,15 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 KS_CHECK(hipMemcpyAsync(s.fb_rng.p, rng.data(), rng.size() * sizeof(long long), hipMemcpyHostToDevice,
                                         st));
                 const int n = (int)std::max<int64_t>(hi0, ncap_prev);
+                KS_CHECK(s.fb_cnt.ensure(1));
+                KS_CHECK(hipMemsetAsync(s.fb_cnt.p, 0, sizeof(unsigned long long), st));
                 hipLaunchKernelGGL(k_fb_reset, dim3(grid_for(std::max(n, 1))), dim3(BLK), 0, st, hi0, (int)ncap_prev,
                                    (int)(rng.size() / 2), (const long long*)s.fb_rng.p, (const int*)s.a_src.p,
-                                   s.saved_flows.p, s.p_slot.p);
+                                   (const unsigned char*)s.a_alive.p, s.saved_flows.p, s.p_slot.p, s.fb_cnt.p);
+                unsigned long long nres = 0;
+                KS_CHECK(hipMemcpyAsync(&nres, s.fb_cnt.p, sizeof(nres), hipMemcpyDeviceToHost, st));
                 KS_CHECK(hipStreamSynchronize(st));   // (rng is a host vector)
+                res.fb_resets = nres;
             }
         }
         int rc = build(s, err);
@@ -4417,11 +4586,14 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // 17.9, 16 14.9 / 16.5, 32 11.6 / 15.4, 48 12.6 / 15.9, 1024 — a single phase at
     // the final ε — 13.4 / 24.4); config 3 and the config-4 rounds are slower at 16
     // and 32, and the cell solver's ladder stays at 8 (config 5 36 ms at 32) — DESIGN §3
-    const int alpha = o.alpha >= 2 ? o.alpha : (!s.cell_layout && nn < 32768) ? 32 : 8;
+    // (the small-graph α and the D below were tuned for the finish: they follow use_prc,
+    // so a graph whose positions do not fit the packed keys keeps the plain schedule)
+    const bool use_pr = o.price_refine != 0;
+    const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && s.m2cap < PK_NONE;
+    const int alpha = o.alpha >= 2 ? o.alpha : (!s.cell_layout && nn < 32768 && use_prc) ? 32 : 8;
     int gi_base = o.gu_interval > 0 ? o.gu_interval : 24;
     gi_base = std::max(2, std::min(MAXB, gi_base)) & ~1;     // even: sweeps end on p0
     const int pr_cap = o.pr_rounds > 0 ? o.pr_rounds : 160;  // price-refinement rounds before giving up
-    const bool use_pr = o.price_refine != 0;
     long long pr_div = 32;   // certify at ε = 1 once ε·pr_div < one (scaled) cost unit
     const bool cycle_log = o.log_cycles != 0;
     const int nhit = s.nhitems;
@@ -4436,7 +4608,6 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     bool pr_failed = false;   // the last phase's refinement did not certify the flow
     // the cycle-cancelling finish replaces the final cost-scaling phase (ks_opts.price_refine
     // 1, the default; 2: the final phase and plain refinement, as before round 5)
-    const bool use_prc = use_pr && o.price_refine == 1 && !s.cell_layout && s.m2cap < PK_NONE;
     // refinement rounds before the final phase takes over (TESTS ONLY, fault_inject bit 5: one batch)
     const int prc_cap = (o.fault_inject & 32) ? 32 : 4096;
     bool prc_tried = false;
@@ -4465,7 +4636,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     {
         const long long D = o.final_div < 0 ? 0
                             : o.final_div > 0 ? o.final_div
-                            : (s.cell_layout || nn < 32768) ? 20 : (use_pr && o.price_refine == 1 ? 24 : 48);
+                            : (s.cell_layout || nn < 32768) ? 20 : (use_prc ? 24 : 48);
         if (D > 0 && use_pr && maxc > 0) {
             long long e = std::max<long long>(1, (mult - 1) / D);
             // the cell solver's ladder is powers of two (α = 8): its arc lengths
@@ -4546,6 +4717,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // graph that cancels the negative cycles it holds. 1 = certified (prices set),
     // 0 = gave up within cap rounds (the final cost-scaling phase follows), < 0 error.
     int prc_cycles = 0, prc_searches = 0;
+    long long prc_rejected = 0;   // nodes / leader walks the searches' union-of-cycles test rejected
     long long solve_units = -1;   // excess units at the solve's first update (cold: the supply)
     unsigned long long gu_prev = 0;   // cycle log: Bellman-Ford relaxations counted so far
     auto prc_refine = [&](int* rounds_used, int cap) -> int {
@@ -4564,17 +4736,39 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         long long* gsum = s.cyc64.p;
         long long* gcap = gsum + nn;
         KS_CHECK(set_eps(1));
-        KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, sizeof(int), st));
+        KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, 2 * sizeof(int), st));   // cyc_done, cyc_rej
         hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, 2);
         const int* done = &s.ctl.p->bf_done;
         // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
         // their least id, every good negative one cancelled in parallel (each kernel
         // returns at once when the refinement has converged)
         int nsearch = 0;
+        // graphs whose parent graph fits one workgroup's LDS search in one launch
+        // (k_cyc_lds) instead of 12–15
+#ifndef KS_EXP_NO_CYC_LDS
+        const bool lds_search = nn <= CYC_LDS_MAX && cyc_lds_bytes(nn) <= s.lds_limit;
+#else
+        const bool lds_search = false;
+#endif
+        if (lds_search) {
+            KS_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cyc_lds<true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)cyc_lds_bytes(nn)));
+            KS_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cyc_lds<false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)cyc_lds_bytes(nn)));
+        }
         auto search = [&]() {
             // three of four searches double only CYC_SHORT times (cycles of up to 128
             // arcs: the ones the finish meets); every fourth covers 2^CYC_LOG
-            const int lg = (nsearch++ % 4 == 3) ? CYC_LOG : CYC_SHORT;
+            // (TESTS ONLY, fault_inject bit 7: every search 5 steps, a window shorter than
+            // the parent chains — their nodes get marked and run into cycles' groups)
+            const int lg = (o.fault_inject & 128) ? 5 : (nsearch++ % 4 == 3) ? CYC_LOG : CYC_SHORT;
+            const int apply_check = (o.fault_inject & 256) ? 0 : 1;
+            if (lds_search) {   // small graphs: the whole search in one workgroup, in LDS
+                const size_t sh = cyc_lds_bytes(nn);
+                if (cpv) k_cyc_lds<true><<<dim3(1), dim3(CYC_LDS_T), sh, st>>>(g, lg, apply_check, bseq, gsum, gcap, gbad);
+                else k_cyc_lds<false><<<dim3(1), dim3(CYC_LDS_T), sh, st>>>(g, lg, apply_check, bseq, gsum, gcap, gbad);
+                return;
+            }
             KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad, indeg);
             for (int d = 0; d < lg; ++d) {
                 if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Jb, Mb, Ja, Ma);
@@ -4586,7 +4780,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
                    gbad, indeg);
             hipLaunchKernelGGL(k_cyc_check, dim3(ngrid), dim3(BLK), 0, st, nn, done, (const int*)J0, MK,
-                               (const int*)onc, (const int*)indeg, gbad);
+                               (const int*)onc, (const int*)indeg, gbad, apply_check, &s.ctl.p->cyc_rej);
             KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
                    (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
         };
@@ -4616,6 +4810,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         ms_pr += ev_ms(s.ev[6], s.ev[7]);
         KS_CHECK(read_ctl());
         prc_cycles += s.h_ctl->cyc_done;
+        prc_rejected += s.h_ctl->cyc_rej;
         *rounds_used = used;
         if (cycle_log)
             std::fprintf(stderr, "cycle-cancelling refinement: %s after %d rounds, %d searches, %d cycles cancelled\n",
@@ -4931,12 +5126,17 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // TESTS ONLY (fault_inject bit 4): the middle cell gives up after 40 operations
         a.fault_cell = (o.fault_inject & 16) && mode == 0 ? ncells / 2 : -1;
         a.fault_ops = 40;
+        a.cyc_lg = (o.fault_inject & 128) ? 5 : 10;   // (ks_cell.hip CYC_LOG)
         KS_CHECK(hipEventRecord(s.kev[2], st));
-        {   // a launch the device refuses (e.g. its LDS) → the multi-kernel engine instead
-            const hipError_t le = cell_launch(a, s.cl_bad.p, s.lds_limit, st);
+        {   // a launch the device refuses (its LDS) → the multi-kernel engine instead; any
+            // other launch error is reported (it used to disable the cell solver)
+            bool refused = false;
+            const hipError_t le = cell_launch(a, s.cl_bad.p, s.lds_limit, st, &refused);
             if (le != hipSuccess) {
                 (void)hipGetLastError();
-                return (int)CS_RANGE;
+                if (refused) return (int)CS_RANGE;
+                err = std::string("cell solver launch: ") + hipGetErrorString(le);
+                return KS_E_DEVICE;
             }
         }
         KS_CHECK(hipEventRecord(s.kev[3], st));
@@ -4958,6 +5158,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             cell_ctr[3] += o.relabels;
             cell_ctr[4] += o.gu_scans;
             prc_cycles += o.cycles;
+            prc_rejected += o.rejected;
             cticks_max = std::max<unsigned long long>(cticks_max, o.ticks);
             cticks_sum += o.ticks;
         }
@@ -5274,6 +5475,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.cell_ticks_sum = cticks_sum;
     res.status = status;
     res.cycles_cancelled = (uint64_t)prc_cycles;
+    res.cycles_rejected = (uint64_t)prc_rejected;
     KS_CHECK(hipMemsetAsync(s.n_cshift.p, 0, s.nstore * sizeof(unsigned long long), st));
     if (status == KS_OK) {
         KS_CHECK(hipMemsetAsync(s.n_fresh.p, 0, s.nstore, st));

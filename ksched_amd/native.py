@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "ks_batch_load", "ks_batch_solve", "ks_batch_gather",
     "ks_batch_slots", "ks_batch_owner", "ks_batch_block_len", "ks_batch_unpack",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 KS_DELTA_PLACE, KS_DELTA_PREEMPT, KS_DELTA_MIGRATE, KS_DELTA_NOOP = 0, 1, 2, 3
 KS_COST_SET, KS_COST_ADD = 0, 1
 
@@ -69,10 +69,11 @@ class KsResult(C.Structure):
                 ("fs_launches", C.c_uint64), ("ms_fs_kernels", C.c_double), ("fwd_updates", C.c_uint64),
                 ("cells", C.c_int32), ("compact", C.c_int32), ("ms_cell_kernel", C.c_double),
                 ("cell_ticks_max", C.c_uint64), ("cell_ticks_sum", C.c_uint64), ("fs_arc_scans", C.c_uint64),
-                ("cell_fallbacks", C.c_uint64), ("cycles_cancelled", C.c_uint64), ("reserved2", C.c_uint64 * 1)]
+                ("cell_fallbacks", C.c_uint64), ("cycles_cancelled", C.c_uint64), ("fb_resets", C.c_uint64),
+                ("cycles_rejected", C.c_uint64), ("reserved3", C.c_uint64 * 3)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "reserved2")}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "reserved3")}
         names = ("build", "saturate", "cycles", "price_refine", "verify", "total")
         d["ms"] = dict(zip(names, list(self.ms_phase)))
         return d
@@ -103,9 +104,21 @@ def lib_path() -> str:
     return _build.variant_path(tag) if tag else _build.LIB
 
 
-def load(build_if_missing: bool = True):
-    """Load the in-tree library (building it with hipcc if absent and allowed)."""
+_VARIANTS: dict = {}
+
+
+def load(build_if_missing: bool = True, variant: str | None = None):
+    """Load the in-tree library (building it with hipcc if absent and allowed).
+    variant: an in-tree build of it, ksched_amd/libksmcmf_<variant>.so (tests use
+    the fake-communicator build "fakecomm", _build.build_fake_comm)."""
     global _LIB
+    if variant is not None:
+        if variant not in _VARIANTS:
+            path = _build.variant_path(variant)
+            if not os.path.exists(path):
+                raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
+            _VARIANTS[variant] = _bind(path)
+        return _VARIANTS[variant]
     if _LIB is not None:
         return _LIB
     path = lib_path()
@@ -113,6 +126,11 @@ def load(build_if_missing: bool = True):
         if not build_if_missing:
             raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
         _build.build()
+    _LIB = _bind(path)
+    return _LIB
+
+
+def _bind(path: str):
     if os.environ.get("KS_PRELOAD_TORCH", "1") != "0":
         # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
         # libamdhip64.so.7) and links it by file name, so if the library loaded
@@ -161,7 +179,6 @@ def load(build_if_missing: bool = True):
     L.ks_scheduling_deltas.argtypes = [V, C.c_int, V, C.c_size_t, P(C.c_size_t)]
     L.ks_update_unsched_costs.argtypes = [V, V, C.c_size_t, C.c_int32, C.c_int64, C.c_int64, P(C.c_size_t)]
     L.ks_topology_stats.argtypes = [V, C.c_uint64, V, V, C.c_size_t, V, V, C.c_size_t, P(C.c_size_t)]
-    _LIB = L
     return L
 
 
@@ -347,8 +364,8 @@ class Batch:
     process-per-GPU job (uid from Batch.unique_id() on rank 0)."""
 
     def __init__(self, devices=None, device: int = 0, world: int = 1, rank: int = 0, uid: bytes | None = None,
-                 **opts):
-        self._L = load()
+                 variant: str | None = None, **opts):
+        self._L = load(variant=variant)   # variant: an in-tree test build (tests: "fakecomm")
         self.opts = default_opts(**opts)
         if uid is None:
             devs = list(devices if devices is not None else [device])

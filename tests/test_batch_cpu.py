@@ -132,8 +132,8 @@ def test_gather_has_no_early_return_after_the_status_all_reduce():
     returns): a failing rank must never leave its peers waiting in ncclSend."""
     src = open(os.path.join(os.path.dirname(HERE), "ksched_amd", "csrc", "ks_batch.hip")).read()
     body = src[src.index("int ks_batch_gather("):]
-    a = body.index("rccl().AllReduce(")
-    g = body.index("const ncclResult_t ge = rccl().GroupEnd();", body.index("// 3. one group"))
+    a = body.index("b->nccl->AllReduce(")
+    g = body.index("const ncclResult_t ge = b->nccl->GroupEnd();", body.index("// 3. one group"))
     seg = body[a:g]
     # the only exits in between: the all-reduce's own error (after its GroupEnd) and
     # the agreed error of every rank (the all-reduce's result), both before any send
@@ -143,3 +143,62 @@ def test_gather_has_no_early_return_after_the_status_all_reduce():
     send = seg.index("// 3. one group")
     assert all(seg.index(e) < send for e in exits), exits
     assert "hipMalloc" not in seg[send:] and "KB_TRY" not in seg[send:]
+
+
+# --- tests/fake_comm: the world-2 rehearsal library checks the protocol it runs ---
+def _fake_comm():
+    """The fake communicator's entry points, from the TEST build of the library
+    (libksmcmf_fakecomm.so; built here if missing). The shipped library must not
+    contain them."""
+    import ctypes as C
+    from ksched_amd import _build
+    lib = C.CDLL(_build.build_fake_comm())
+    base = C.CDLL(_build.LIB)
+    assert not hasattr(base, "ks_fake_ncclGroupEnd"), "the shipped library carries the fake communicator"
+
+    class F:
+        pass
+    f = F()
+    for name in ("CommInitAll", "GroupStart", "GroupEnd", "AllReduce", "Send", "Recv", "CommDestroy"):
+        fn = getattr(lib, "ks_fake_nccl" + name)
+        fn.restype = C.c_int
+        setattr(f, "nccl" + name, fn)
+    return C, f
+
+
+NCCL_INVALID_USAGE = 5   # rccl.h ncclInvalidUsage
+NCCL_INT64, NCCL_MIN = 4, 3
+
+
+def test_fake_comm_refuses_a_one_sided_all_reduce():
+    """A rank that skipped the status all-reduce would hang a real RCCL job; the
+    fake communicator (tests/fake_comm, in the test build the world-2 GPU tests
+    use) reports it as ncclInvalidUsage at GroupEnd instead — before any device
+    call, so it runs here."""
+    C, lib = _fake_comm()
+    comms = (C.c_void_p * 2)()
+    devs = (C.c_int * 2)(0, 0)
+    assert lib.ncclCommInitAll(comms, 2, devs) == 0
+    buf = C.c_void_p(0x1000)
+    assert lib.ncclGroupStart() == 0
+    assert lib.ncclAllReduce(buf, buf, 1, NCCL_INT64, NCCL_MIN, C.c_void_p(comms[0]), None) == 0
+    assert lib.ncclGroupEnd() == NCCL_INVALID_USAGE
+    # outside a group: refused (ks_batch always groups)
+    assert lib.ncclAllReduce(buf, buf, 1, NCCL_INT64, NCCL_MIN, C.c_void_p(comms[0]), None) == NCCL_INVALID_USAGE
+    for c in comms:
+        assert lib.ncclCommDestroy(C.c_void_p(c)) == 0
+
+
+def test_fake_comm_refuses_an_unmatched_send():
+    C, lib = _fake_comm()
+    comms = (C.c_void_p * 2)()
+    assert lib.ncclCommInitAll(comms, 2, (C.c_int * 2)(0, 0)) == 0
+    buf = C.c_void_p(0x1000)
+    assert lib.ncclGroupStart() == 0
+    assert lib.ncclSend(buf, 8, NCCL_INT64, 0, C.c_void_p(comms[1]), None) == 0   # rank 1 → 0, no receive posted
+    assert lib.ncclGroupEnd() == NCCL_INVALID_USAGE
+    assert lib.ncclGroupStart() == 0
+    assert lib.ncclRecv(buf, 8, NCCL_INT64, 1, C.c_void_p(comms[0]), None) == 0   # a receive nobody sends
+    assert lib.ncclGroupEnd() == NCCL_INVALID_USAGE
+    for c in comms:
+        assert lib.ncclCommDestroy(C.c_void_p(c)) == 0

@@ -237,25 +237,34 @@ def test_failing_cell_falls_back_alone():
     """a cell that gives up in the cell solver (injected: ks_opts
     fault_inject bit 4 stops the middle cell of the batch after 40 operations with
     CS_NOCONV) is re-solved on the multi-kernel engine; the other cells' optima are
-    kept, the solve returns KS_OK, and every cell equals the CPU oracle."""
+    kept, the solve returns KS_OK, and every cell equals the CPU oracle. ADVICE r5:
+    the failing cell really restarts cold — k_fb_reset reports exactly the middle
+    graph's live arcs plus node slots as reset (ks_result.fb_resets), so a wrong
+    node range (which a warm restart from the partial flow would hide, since it
+    reaches the same optimum) fails here."""
     graphs = [gen.quincy(2_000, 200, 10, 20, 1500 + i) for i in range(6)]
     want = [ko.cost_scaling(g)[1:3] for g in graphs]
+    mid = graphs[len(graphs) // 2]
     b = native.Batch(devices=[0], fault_inject=16)
     try:
         b.load(graphs)
         res = b.solve()
         assert res[0].raw["solver"] == 1 and res[0].raw["cells"] == 6
         assert res[0].raw["cell_fallbacks"] == 1
+        assert res[0].raw["warm_started"] == 1          # the converged cells' optima are carried
+        assert res[0].raw["fb_resets"] == mid.n + mid.m
         pu, cost, flow = b.gather(2_000)
         assert list(zip(cost.tolist(), flow.tolist())) == want
         for i in (2, 3):
             g = graphs[i]
             tasks = np.nonzero(g.ntype == 1)[0] + 1
             check_mapping(g, {int(t): int(p) for t, p in zip(tasks, pu[i]) if p})
-        # the next solve of the same batch runs in the cell solver again (no fault on
-        # a re-solve: the fault hits the first attempt of each solve the same way)
+        # the next solve of the same batch starts in the cell solver again; the fault
+        # hits the middle cell's first attempt in every solve, so it falls back the
+        # same way and gives the same costs
         res = b.solve()
         assert res[0].raw["cell_fallbacks"] == 1
+        assert res[0].raw["fb_resets"] == mid.n + mid.m
         _, cost2, _ = b.gather(2_000)
         assert cost2.tolist() == cost.tolist()
     finally:

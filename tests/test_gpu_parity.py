@@ -317,7 +317,8 @@ def test_tail_updates_do_not_change_the_optimum(opts):
     tail), and down to ε = 1 without price refinement; the bounded global update
     off. Same optimum as the oracle, flow re-verified, on a config-2-sized cell
     and random graphs (several deficits, lower bounds, parallel paths)."""
-    # α 8: a config-2 solve at its default α (16) has no coarse phase with a tail
+    # α 8: a config-2 solve at its default α (32 on the engine below 32,768 nodes)
+    # has no coarse phase with a tail
     with native.Context(0, cell_nodes=-1, alpha=8, **opts) as c2:   # the engine's tail updates
         g = gen.quincy(10_000, 1_000, 25, 100, 2)
         st, c, fv, _, _ = ko.ssp(g)
@@ -453,3 +454,67 @@ def test_cycle_cancelling_finish(path, opts):
         assert cc == 0
     elif not opts.get("fault_inject"):
         assert cc > 0, "no negative cycle was cancelled on three config-2 cells"
+
+
+def _search_graphs(with_config3):
+    """Three config-2 cells (seeds 2, 7, 11) and, on the engine, config 3 — with the
+    oracle's (cost, flow) from the committed goldens or the cost-scaling oracle."""
+    out = []
+    seeds = [("config2", 2), ("config2", 7), ("config2", 11)] + ([("config3", 3)] if with_config3 else [])
+    gold = {(tuple(e["params"]), e["seed"]): e for e in load_goldens() if e["family"] == "quincy"}
+    for name, seed in seeds:
+        T, M, R, J, _ = gen.CONFIGS[name]
+        g = gen.quincy(T, M, R, J, seed)
+        e = gold.get(((T, M, R, J), seed))
+        if e is not None:
+            want = (e["cost"], e["flow"])
+        else:
+            st, c, fv, _ = ko.cost_scaling(g)
+            assert st == 0
+            want = (c, fv)
+        out.append((g, want))
+    return out
+
+
+@pytest.mark.parametrize("path", ["engine", "cell"])
+def test_cycle_search_rejects_chains(path):
+    """the finish's union-of-cycles test on its rejection path.
+    fault_inject bit 7 shortens every parent-graph search to a 32-node window, far
+    shorter than the refinement's parent chains, so chain nodes get marked and run
+    into cycles' groups (the case that once pushed along a chain and returned
+    3,257,657 with KS_OK). The test must reject them (cycles_rejected > 0) and the
+    cycles it keeps must still be cancelled: every solve returns the oracle's cost
+    with no recovery and no KS_E_VERIFY — on three config-2 cells and config 3 on
+    the engine (k_cyc_check), and on the config-2 cells in the cell solver (whose
+    leader walk must close on itself). Config 3 is beyond the cell solver's size."""
+    cell = path == "cell"
+    cc = rej = 0
+    with native.Context(0, cell_nodes=20_000 if cell else -1, fault_inject=128) as c2:
+        for g, (cost, flow) in _search_graphs(with_config3=not cell):
+            r = solve_and_check(c2, g, cost, flow)
+            assert r.raw["solver"] == (1 if cell else 0)
+            assert r.raw["recoveries"] == 0
+            cc += r.raw["cycles_cancelled"]
+            rej += r.raw["cycles_rejected"]
+    assert cc > 0, "no cycle was cancelled through the short window"
+    assert rej > 0, "the short window never produced a group the test had to reject"
+
+
+def test_cycle_search_without_the_check_fails_loudly():
+    """The same short window with the engine's union-of-cycles test only counting
+    (fault_inject bit 8): groups joined by a chain are then pushed along, which
+    breaks conservation. The verifier (conservation from the downloaded flows) must
+    turn that into KS_E_VERIFY on at least one graph — and no solve may return a
+    cost other than the oracle's."""
+    failed = 0
+    with native.Context(0, cell_nodes=-1, fault_inject=128 | 256) as c2:
+        for g, (cost, flow) in _search_graphs(with_config3=True):
+            c2.load_graph(g)
+            try:
+                r = c2.solve()
+            except native.KsError as e:
+                assert e.code == native.KS_E_VERIFY, str(e)
+                failed += 1
+                continue
+            assert (r.cost, r.flow) == (cost, flow)
+    assert failed > 0, "no chain was pushed along: the unchecked search never met the bad case"

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of solver options (ks_opts fields) on one GPU: config-3 solves
+"""Interleaved A/B of solver options (ks_opts fields) — or, with --variant TAG, of the
+default library against libksmcmf_TAG.so (same options) — on one GPU: config-3 solves
 and config-4 churn rounds, every result checked against the golden / the other
 variant. Each variant has its own context on the same graph; solves alternate
 A, B, A, B … so clock and thermal drift hit both alike.
@@ -35,14 +36,28 @@ def main():
     ap.add_argument("--solves", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--config", default="config3", help="solves: gen.CONFIGS name (config2, config3)")
+    ap.add_argument("--variant", default="", help="b runs libksmcmf_<variant>.so (a: the default library)")
     a = ap.parse_args()
     va, vb = parse(a.a), parse(a.b)
+    libs = {}
+    if a.variant:
+        os.environ.pop("KS_LIB_VARIANT", None)
+        native._LIB = None
+        libs["a"] = native.load()
+        os.environ["KS_LIB_VARIANT"] = a.variant
+        native._LIB = None
+        libs["b"] = native.load()
+
+    def make(k, v):
+        if libs:
+            native._LIB = libs[k]
+        return native.Context(0, **v)
     T, M, R, J, seed = gen.CONFIGS["config3"]
     out = {"a": va, "b": vb}
     if a.solves:
         g = gen.quincy(*gen.CONFIGS[a.config])
         ref = None
-        ctx = {k: native.Context(0, **v) for k, v in (("a", va), ("b", vb))}
+        ctx = {k: make(k, v) for k, v in (("a", va), ("b", vb))}
         for c in ctx.values():
             c.load_graph(g)
             c.solve()
@@ -68,7 +83,7 @@ def main():
         # one churn stream (driven by variant a's mappings) applied to both contexts:
         # the same graph every round, so the costs must agree exactly
         cell = churn.Cell(T, M, R, J, seed)
-        ctx = {k: native.Context(0, **v) for k, v in (("a", va), ("b", vb))}
+        ctx = {k: make(k, v) for k, v in (("a", va), ("b", vb))}
         g = cell.graph()
         for k in ("a", "b"):
             ctx[k].load_graph(g)

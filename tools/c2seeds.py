@@ -20,7 +20,10 @@ def parse(spec):
 T, M, R, J, _ = gen.CONFIGS["config2"]
 seeds = [2, 7, 11] + list(range(1000, 1009))
 graphs = [gen.quincy(T, M, R, J, s) for s in seeds]
-for spec in sys.argv[1:]:
+_gold = {e["seed"]: e["cost"] for e in __import__("json").load(open(__import__("os").path.join(
+    __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))),
+    "tests", "golden", "goldens.json")))["graphs"] if e["family"] == "quincy" and e["params"] == [T, M, R, J]}
+for spec in sys.argv[1:] or [""]:
     opts = parse(spec)
     cells = opts.pop("cell", 0)
     ms, costs = [], []
@@ -35,5 +38,8 @@ for spec in sys.argv[1:]:
                 ts.append(1e3 * (time.perf_counter() - t0))
             ms.append(float(np.median(ts)))
             costs.append(r.cost)
-    print(f"{spec or 'default':>24}: median {np.median(ms):6.2f} ms, mean {np.mean(ms):6.2f}, max {max(ms):6.2f}; "
+            s_ = seeds[len(costs) - 1]
+            assert s_ not in _gold or _gold[s_] == r.cost, (s_, r.cost, _gold[s_])
+    tag = __import__("os").environ.get("KS_LIB_VARIANT", "")
+    print(f"{tag + ':' + (spec or 'default'):>24}: median {np.median(ms):6.2f} ms, mean {np.mean(ms):6.2f}, max {max(ms):6.2f}; "
           f"per seed {' '.join(f'{x:.1f}' for x in ms)}; costs {costs[:3]}", flush=True)

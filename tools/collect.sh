@@ -1,8 +1,9 @@
 #!/bin/bash
-# Copy a round-5 measurement (tools/gpu_r05_final.sh TAG) from gpurun_out/ into
+# Copy a round's measurement (tools/gpu_round.sh TAG) from gpurun_out/ into
 # profiles/ under PREFIX: bench lines, per-workload PMC traffic (pmc_traffic.py,
-# calibration carried from profiles/r03m_pmc_traffic.json) and kernel stats, pytest log.
-# Usage: collect_r04.sh TAG PREFIX DATE
+# calibration carried from profiles/r03m_pmc_traffic.json) and kernel stats, the GPU
+# suite log and smoke output.
+# Usage: collect.sh TAG PREFIX DATE
 set -e
 TAG=$1; P=$2; DATE=$3
 IN=gpurun_out/$TAG
@@ -15,4 +16,5 @@ for wl in config3 config2 config4 config5; do
     fi
 done
 [ -f gpurun_out/$TAG/pytest_gpu.log ] && cp gpurun_out/$TAG/pytest_gpu.log "profiles/${P}_pytest_gpu.log"
+[ -f gpurun_out/$TAG/smoke.log ] && cp gpurun_out/$TAG/smoke.log "profiles/${P}_smoke.log"
 ls -la profiles/${P}_*

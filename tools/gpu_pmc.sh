@@ -2,7 +2,7 @@
 # PMC passes over one bench run of a workload, one rocprofv3 run per pass
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass; TCC holds 4 counters, TA 2),
 # then a kernel-trace pass for the per-kernel device time. The trace pass runs
-# the bench line's own arguments (TARGS, as tools/gpu_r04_final.sh runs them), so
+# the bench line's own arguments (TARGS, as tools/gpu_round.sh runs them), so
 # its per-kernel averages cover the same launch mix as the event-timed line.
 # Usage: gpu_pmc.sh TAG [config3|config2|config4|config5] [all|trace]
 set -o pipefail
