@@ -156,6 +156,12 @@ struct Ctl {
     long long u_exc_rep;
     int fs_completed;      // forward updates completed (whole solve)
     int fs_moved_cyc;      // units the traces of this cycle moved
+    // device-clock timing (s_memrealtime, 100 MHz) where a HIP event between two
+    // kernels would cost a ~5.7 µs gap of its own (profiles/r06_*_gaps):
+    unsigned long long t_sw0;       // the cycle's first sweep started
+    unsigned long long t_end;       // k_cycle_end started (= the last sweep ended)
+    unsigned long long t_srch;      // the finish's running parent-graph search started (0: none)
+    unsigned long long srch_ticks;  // the finish's searches so far (subtracted from its batches' spans)
 };
 
 struct HItem {
@@ -1293,6 +1299,7 @@ __device__ __forceinline__ void sweep_win(const DG& g, const Front& N, int w, un
 
 template <bool CP>
 __global__ __launch_bounds__(BLK) void k_sweep(DG g, int pos, int seq) {
+    if (pos == 0 && blockIdx.x == 0 && threadIdx.x == 0) g.ctl->t_sw0 = __builtin_amdgcn_s_memrealtime();
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < g.nheavy; h += BLK) g.sf[(seq + 2) % 3].hub[h] = 0;
     // The preceding global update was applied (c_done) and the frontier is
@@ -1605,6 +1612,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
 // (bf_seq0, set by the init kernel); ≥ 0: as given.
 template <int PR, bool CP>
 __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) {
+    const unsigned long long t_entry = PR == 2 ? __builtin_amdgcn_s_memrealtime() : 0;
     const int dense = dense_arg >= 0 ? dense_arg : (seq == g.ctl->bf_seq0 ? 1 : 0);
     __shared__ long long hub_min[HUB_LDS];
     if (blockIdx.x == 0) {
@@ -1720,6 +1728,10 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
     }
     if (__any(out) && lane_id() == 0) g.ctl->bfa[(seq + 1) % 3] = 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // block 0 is a hub block or a window block: done/any are final here
+        if (PR == 2 && g.ctl->t_srch) {   // the finish: the search before this round ended when it started
+            g.ctl->srch_ticks += t_entry - g.ctl->t_srch;
+            g.ctl->t_srch = 0;
+        }
         if (!done && (dense || any)) {
             atomicAdd(g.ctr + C_BFROUND, 1ULL);
             g.ctl->bf_count += 1;
@@ -1837,8 +1849,10 @@ __global__ void k_pr_init(DG g, int seq0, int from_p) {
 // transfer would drain the queue around it: ~65 µs of idle GPU per cycle).
 __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
     static_assert(sizeof(Ctl) % 4 == 0, "Ctl is copied as words");
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         if (!fwd) g.ctl->gu_pending = g.ctl->bf_done ? 0 : 1;   // (forward: k_fs_end)
+        g.ctl->t_end = t;
     }
     __syncthreads();
     const int* src = reinterpret_cast<const int*>(g.ctl);
@@ -1860,6 +1874,22 @@ __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
 
 // max finite distance (only once the update converged); cleans the sweep
 // frontiers and flags the apply step and the sweeps write.
+// The finish's batch end: closes the running search's time and copies the control
+// block into pinned host memory (no copy-engine transfer: that drains the queue).
+__global__ void k_prc_snap(DG g, Ctl* host) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && g.ctl->t_srch) {
+        g.ctl->srch_ticks += t - g.ctl->t_srch;
+        g.ctl->t_srch = 0;
+    }
+    __syncthreads();
+    const int* src = reinterpret_cast<const int*>(g.ctl);
+    int* dst = reinterpret_cast<int*>(host);
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += blockDim.x)
+        __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+}
+
 __global__ void k_gu_max(DG g) {
     __shared__ long long sh[WPB];
     clear_fronts(g, g.sf);
@@ -2576,20 +2606,20 @@ constexpr int CYC_PERIODS = 3;            // rounds + search periods per host ch
 constexpr long long kPrcUnitsDiv = 4;   // an earlier finish (run_phase prc_early)
 
 // The parent of every node (itself for a root) from its key's position a (the
-// parent v is the head of a's reverse); its own id as the window minimum; the
-// per-group sums reset.
+// parent v is the head of a's reverse); the jump word (node one step ahead, least
+// id over the one-node window = its own id); the per-group sums reset.
 template <bool CP>
-__global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* __restrict__ M,
-                          int* __restrict__ onc, int* __restrict__ R, long long* __restrict__ gsum,
-                          long long* __restrict__ gcap, int* __restrict__ gbad, int* __restrict__ indeg) {
+__global__ void k_cyc_par(DG g, int* __restrict__ J0, int2* __restrict__ JM, int* __restrict__ onc,
+                          int* __restrict__ R, long long* __restrict__ gsum, long long* __restrict__ gcap,
+                          int* __restrict__ gbad, int* __restrict__ indeg) {
     if (g.ctl->bf_done) return;   // the refinement converged: no search
+    if (blockIdx.x == 0 && threadIdx.x == 0) g.ctl->t_srch = __builtin_amdgcn_s_memrealtime();
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         const long long a = atom_load(&g.dist[ni(u)]) & PK_NONE;
         int v = (int)u;
         if (a != PK_NONE) v = PL<CP>::head(g, PL<CP>::rev(g, (int)a));
         J0[u] = v;
-        J[u] = v;
-        M[u] = (int)u;
+        JM[u] = make_int2(v, (int)u);
         R[u] = (int)a;
         onc[u] = 0;
         gsum[u] = 0;
@@ -2598,24 +2628,28 @@ __global__ void k_cyc_par(DG g, int* __restrict__ J0, int* __restrict__ J, int* 
         indeg[u] = 0;
     }
 }
-// one doubling step: 2^k → 2^(k+1) steps ahead, and the least id over them
-__global__ void k_cyc_dbl(int n, const int* __restrict__ done, const int* __restrict__ Ji,
-                          const int* __restrict__ Mi, int* __restrict__ Jo, int* __restrict__ Mo) {
+// One jump step: a window of w nodes → F·w (F jumps of the previous step chained;
+// F = 4 per launch where the window allows, 2 for an odd power of two: a search
+// covers 128 steps in 4 launches, 1,024 in 5, instead of 7 and 10 doublings). The
+// jump word packs the node w steps ahead and the least id over the window. On the
+// search's last step (mark) every node a window ahead of another is marked — it
+// lies on a cycle, or (past the window) on a chain, which the union-of-cycles test
+// rejects; roots (their own parent) are skipped.
+template <int F>
+__global__ void k_cyc_jump(int n, const int* __restrict__ done, const int2* __restrict__ JMi,
+                           int2* __restrict__ JMo, int mark, const int* __restrict__ J0, int* __restrict__ onc) {
     if (*done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
-        const int j = Ji[u];
-        Jo[u] = Ji[j];
-        Mo[u] = min(Mi[u], Mi[j]);
-    }
-}
-// every node CYC_WALK steps ahead of some node lies on a cycle (the refinement's
-// parent chains are far shorter than CYC_WALK); roots (their own parent) are skipped
-__global__ void k_cyc_mark(int n, const int* __restrict__ done, const int* __restrict__ JK,
-                           const int* __restrict__ J0, int* __restrict__ onc) {
-    if (*done) return;
-    for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK) {
-        const int x = JK[u];
-        if (J0[x] != x) onc[x] = 1;
+        int2 c = JMi[u];
+        int mn = c.y;
+#pragma unroll
+        for (int f = 1; f < F; ++f) {
+            const int2 x = JMi[c.x];
+            mn = min(mn, x.y);
+            c.x = x.x;
+        }
+        JMo[u] = make_int2(c.x, mn);
+        if (mark && J0[c.x] != c.x) onc[c.x] = 1;
     }
 }
 // Each cycle node adds its parent arc (u → v, the reverse of position R[u]) to its
@@ -2623,18 +2657,20 @@ __global__ void k_cyc_mark(int n, const int* __restrict__ done, const int* __res
 // most CYC_WALK nodes: cost sum, bottleneck residual. A group whose nodes disagree
 // on the group (a longer cycle) or whose arc is not residual is marked bad.
 template <bool CP>
-__global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
+__global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int2* __restrict__ MK, const int* __restrict__ onc,
                             const int* __restrict__ R, long long* __restrict__ gsum, long long* __restrict__ gcap,
                             int* __restrict__ gbad, int* __restrict__ indeg) {
     if (g.ctl->bf_done) return;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         if (!onc[u] || J0[u] == (int)u) continue;
-        const int m = MK[u], mn = MK[J0[u]];
-        if (mn != m || !onc[J0[u]]) {   // (a parent off every cycle: a chain, not a cycle)
-            gbad[m] = 1;
-            gbad[mn] = 1;
-        }
-        atomicAdd(&indeg[J0[u]], 1);
+        const int m = MK[u].y, mn = MK[J0[u]].y;
+        // a parent off the group (another group, or unmarked): u's arc leaves the
+        // group, which is then no union of cycles. The parent's group is not blamed:
+        // it counts only its own members' pointers (a chain of another group that
+        // runs into a cycle leaves the cycle's group intact, and cancelling it moves
+        // nothing the chain's group owns).
+        if (mn != m || !onc[J0[u]]) gbad[m] = 1;
+        else atomicAdd(&indeg[J0[u]], 1);
         const Pos q = PL<CP>::ld_nr(g, R[u]);
         const long long res = q.ucap - q.rcap;   // residual of the reverse: the arc u → v
         if (res <= 0) gbad[m] = 1;
@@ -2643,19 +2679,21 @@ __global__ void k_cyc_group(DG g, const int* __restrict__ J0, const int* __restr
     }
 }
 // A group is a union of cycles only if each of its nodes has exactly one member
-// pointing at it: a chain longer than the doubling window (its nodes marked too)
-// that runs into a cycle gives the junction two, its first node none, and the
-// group is dropped (pushing along a chain would break conservation).
+// of the group pointing at it (and every member's parent is a member, k_cyc_group):
+// each member then has one push out and one push in. A chain longer than the
+// doubling window (its nodes marked too) that joins a cycle's group gives the
+// junction two, its first node none, and the group is dropped (pushing along a
+// chain would break conservation).
 // Such nodes are counted (ctl->cyc_rej); apply = 0 (TESTS ONLY, fault_inject bit 8)
 // counts them without dropping their groups.
 __global__ void k_cyc_check(int n, const int* __restrict__ done, const int* __restrict__ J0,
-                            const int* __restrict__ MK, const int* __restrict__ onc, const int* __restrict__ indeg,
+                            const int2* __restrict__ MK, const int* __restrict__ onc, const int* __restrict__ indeg,
                             int* __restrict__ gbad, int apply, int* __restrict__ rej) {
     if (*done) return;
     int cnt = 0;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < n; u += (long long)gridDim.x * BLK)
         if (onc[u] && J0[u] != (int)u && atom_load_i(&indeg[u]) != 1) {
-            if (apply) gbad[MK[u]] = 1;
+            if (apply) gbad[MK[u].y] = 1;
             ++cnt;
         }
     cnt = (int)wave_sum(cnt);
@@ -2666,7 +2704,7 @@ __global__ void k_cyc_check(int n, const int* __restrict__ done, const int* __re
 // its own parent arc (the arcs of different nodes are different positions), and
 // rejoins the frontier the next refinement round reads (buffer seq).
 template <bool CP>
-__global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int* __restrict__ MK, const int* __restrict__ onc,
+__global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int2* __restrict__ MK, const int* __restrict__ onc,
                            const int* __restrict__ R, const long long* __restrict__ gsum,
                            const long long* __restrict__ gcap, const int* __restrict__ gbad, int seq) {
     if (g.ctl->bf_done) return;
@@ -2674,7 +2712,7 @@ __global__ void k_cyc_push(DG g, const int* __restrict__ J0, const int* __restri
     int out = 0, cyc = 0;
     for (long long u = blockIdx.x * (long long)BLK + threadIdx.x; u < g.n; u += (long long)gridDim.x * BLK) {
         if (!onc[u] || J0[u] == (int)u) continue;
-        const int m = MK[u];
+        const int m = MK[u].y;
         const long long dl = gcap[m];
         if (gbad[m] || gsum[m] >= 0 || dl <= 0 || dl >= INF64) continue;
         const int a = R[u];
@@ -2714,6 +2752,7 @@ __global__ __launch_bounds__(CYC_LDS_T) void k_cyc_lds(DG g, int lg, int apply_c
                                                       long long* __restrict__ gsum, long long* __restrict__ gcap,
                                                       int* __restrict__ gbad) {
     if (g.ctl->bf_done) return;   // the refinement converged: no search
+    if (threadIdx.x == 0) g.ctl->t_srch = __builtin_amdgcn_s_memrealtime();
     extern __shared__ int cyc_sm[];
     const int n = g.n;
     int* J0 = cyc_sm;
@@ -2788,11 +2827,8 @@ __global__ __launch_bounds__(CYC_LDS_T) void k_cyc_lds(DG g, int lg, int apply_c
         const int m = (w & ~CYC_LDS_ON) >> CYC_LDS_IDB;
         const int wp = Wi[p];
         const int mn = (wp & ~CYC_LDS_ON) >> CYC_LDS_IDB;
-        if (mn != m || !(wp & CYC_LDS_ON)) {   // (a parent off every cycle: a chain, not a cycle)
-            gbad[m] = 1;
-            gbad[mn] = 1;
-        }
-        atomicAdd(&Wo[p], 1);
+        if (mn != m || !(wp & CYC_LDS_ON)) gbad[m] = 1;   // u's arc leaves its group (k_cyc_group)
+        else atomicAdd(&Wo[p], 1);
         const int a = (int)(atom_load(&g.dist[ni(u)]) & PK_NONE);
         const Pos q = PL<CP>::ld_nr(g, a);
         const long long res = q.ucap - q.rcap;   // residual of the reverse: the arc u → v
@@ -3234,6 +3270,7 @@ struct EngineImpl {
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     hipEvent_t kev[4] = {};   // kernel-batch timing (price refinement)
+    hipEvent_t fin_ev[4] = {};      // the finish's pipelined batches: [3] its start, [b % 3] batch b's end
     // per-cycle timing, each kind's span bracketing exactly its kernels: [0] before the
     // first Bellman-Ford round, [1] after the last, [2] before the first sweep, [3] after
     // the last sweep; forward cycles: [0]/[1] around each update's search rounds (fev)
@@ -3407,6 +3444,9 @@ struct EngineImpl {
             if (e) (void)hipEventDestroy(e);
         for (auto& e : kev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& e : fin_ev)
+            if (e) (void)hipEventDestroy(e);
+        fb_cnt.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -3552,6 +3592,7 @@ int Engine::init(int device, const ks_opts& opts, std::string& err) {
     }
     for (auto& e : s.ev) KS_CHECK(hipEventCreate(&e));
     for (auto& e : s.kev) KS_CHECK(hipEventCreate(&e));
+    for (auto& e : s.fin_ev) KS_CHECK(hipEventCreate(&e));
     for (auto& c : s.cev)
         for (auto& e : c) KS_CHECK(hipEventCreate(&e));
     for (auto& c : s.fev)
@@ -4724,12 +4765,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         KS_CHECK(hipEventRecord(s.ev[6], st));
         KS_CHECK(s.cyc.ensure((size_t)9 * nn));
         KS_CHECK(s.cyc64.ensure((size_t)2 * nn));
-        int* J0 = s.cyc.p;
-        int* Ja = J0 + nn;
-        int* Jb = Ja + nn;
-        int* Ma = Jb + nn;
-        int* Mb = Ma + nn;
-        int* onc = Mb + nn;
+        int2* JMa = reinterpret_cast<int2*>(s.cyc.p);   // jump words, double-buffered (8-B aligned)
+        int2* JMb = JMa + nn;
+        int* J0 = reinterpret_cast<int*>(JMb + nn);
+        int* onc = J0 + nn;
         int* R = onc + nn;
         int* gbad = R + nn;
         int* indeg = gbad + nn;   // members of its group pointing at a node
@@ -4745,11 +4784,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int nsearch = 0;
         // graphs whose parent graph fits one workgroup's LDS search in one launch
         // (k_cyc_lds) instead of 12–15
-#ifndef KS_EXP_NO_CYC_LDS
         const bool lds_search = nn <= CYC_LDS_MAX && cyc_lds_bytes(nn) <= s.lds_limit;
-#else
-        const bool lds_search = false;
-#endif
         if (lds_search) {
             KS_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cyc_lds<true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)cyc_lds_bytes(nn)));
@@ -4769,40 +4804,93 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 else k_cyc_lds<false><<<dim3(1), dim3(CYC_LDS_T), sh, st>>>(g, lg, apply_check, bseq, gsum, gcap, gbad);
                 return;
             }
-            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, Ja, Ma, onc, R, gsum, gcap, gbad, indeg);
-            for (int d = 0; d < lg; ++d) {
-                if (d & 1) hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Jb, Mb, Ja, Ma);
-                else hipLaunchKernelGGL(k_cyc_dbl, dim3(ngrid), dim3(BLK), 0, st, nn, done, Ja, Ma, Jb, Mb);
+            KS_HOT(cpv, k_cyc_par, ngrid, BLK, st, g, J0, JMa, onc, R, gsum, gcap, gbad, indeg);
+            const int2* JMK = JMa;
+            for (int left = lg, k = 0; left > 0; ++k) {   // ×4 per launch, ×2 for an odd remainder
+                const int2* in = (k & 1) ? JMb : JMa;
+                int2* out = (k & 1) ? JMa : JMb;
+                const int f2 = left >= 2 ? 2 : 1;
+                left -= f2;
+                const int mark = left == 0 ? 1 : 0;
+                if (f2 == 2)
+                    hipLaunchKernelGGL(k_cyc_jump<4>, dim3(ngrid), dim3(BLK), 0, st, nn, done, in, out, mark,
+                                       (const int*)J0, onc);
+                else
+                    hipLaunchKernelGGL(k_cyc_jump<2>, dim3(ngrid), dim3(BLK), 0, st, nn, done, in, out, mark,
+                                       (const int*)J0, onc);
+                JMK = out;
             }
-            const int* JK = (lg & 1) ? Jb : Ja;
-            const int* MK = (lg & 1) ? Mb : Ma;
-            hipLaunchKernelGGL(k_cyc_mark, dim3(ngrid), dim3(BLK), 0, st, nn, done, JK, (const int*)J0, onc);
-            KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R, gsum, gcap,
+            KS_HOT(cpv, k_cyc_group, ngrid, BLK, st, g, (const int*)J0, JMK, (const int*)onc, (const int*)R, gsum, gcap,
                    gbad, indeg);
-            hipLaunchKernelGGL(k_cyc_check, dim3(ngrid), dim3(BLK), 0, st, nn, done, (const int*)J0, MK,
+            hipLaunchKernelGGL(k_cyc_check, dim3(ngrid), dim3(BLK), 0, st, nn, done, (const int*)J0, JMK,
                                (const int*)onc, (const int*)indeg, gbad, apply_check, &s.ctl.p->cyc_rej);
-            KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, MK, (const int*)onc, (const int*)R,
+            KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, JMK, (const int*)onc, (const int*)R,
                    (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
         };
-        // batches of CYC_PERIODS × (CYC_EVERY rounds + a search) per host check
-        int used = 0, ok = 0;
-        for (int batch = 0; used < cap; ++batch) {
-            KS_CHECK(hipEventRecord(s.kev[0], st));
-            for (int per = 0; per < (batch == 0 ? 1 : CYC_PERIODS) && used < cap; ++per) {
-                const int k = std::min(batch == 0 ? 2 * CYC_EVERY : CYC_EVERY, cap - used);
-                bf_rounds(2, k, batch == 0);
+        // Batches of CYC_PERIODS × (CYC_EVERY rounds + a search), pipelined two deep:
+        // batch b+1 is enqueued before the host waits for batch b's control snapshot
+        // (k_prc_snap, into pinned memory), so the GPU does not idle through the
+        // host's round trip (~27 µs per batch with a copy-engine read, r06 traces).
+        // Once the refinement has converged, every kernel of the batch in flight
+        // exits at once. A batch's Bellman-Ford time is its event span less its
+        // searches (device clock: k_cyc_par / k_cyc_lds to the next round's start).
+        // One event per batch, after its snapshot: batch b's span runs from batch
+        // b−1's event (the first: fin_ev[3]) — two events back to back cost a gap each.
+        int used = 0, ok = 0, nb = 0;   // nb: batches enqueued
+        unsigned long long srch_seen = 0;
+        KS_CHECK(hipEventRecord(s.fin_ev[3], st));
+        auto end_ev = [&](int b) { return s.fin_ev[b % 3]; };
+        auto start_ev = [&](int b) { return b == 0 ? s.fin_ev[3] : s.fin_ev[(b - 1) % 3]; };
+        auto enqueue_batch = [&](int slot) -> hipError_t {
+            const int b = nb++;
+            for (int per = 0; per < (b == 0 ? 1 : CYC_PERIODS) && used < cap; ++per) {
+                const int k = std::min(b == 0 ? 2 * CYC_EVERY : CYC_EVERY, cap - used);
+                bf_rounds(2, k, b == 0);
                 used += k;
                 search();
                 ++prc_searches;
             }
-            KS_CHECK(hipEventRecord(s.kev[1], st));
+            hipLaunchKernelGGL(k_prc_snap, dim3(1), dim3(128), 0, st, g, s.d_cyc[slot]);
+            return hipEventRecord(end_ev(b), st);
+        };
+        auto batch_time = [&](int b) {   // → ms_bf_k
+            const Ctl* hc = s.h_cyc[b & 1];
+            const double span = ev_ms(start_ev(b), end_ev(b));
+            const double srch = hc->srch_ticks > srch_seen ? (double)(hc->srch_ticks - srch_seen) / 1e5 : 0.0;
+            srch_seen = std::max(srch_seen, hc->srch_ticks);
+            ms_bf_k += std::max(0.0, span - srch);
+            return span;
+        };
+        KS_CHECK(enqueue_batch(0));
+        int done_b = 0;   // batches whose snapshot the host has read
+        for (int batch = 0;; ++batch) {
+            const int slot = batch & 1;
+            const bool more = used < cap;
+            if (more) KS_CHECK(enqueue_batch(slot ^ 1));
+            KS_CHECK(hipEventSynchronize(end_ev(batch)));
+            ++done_b;
+            const Ctl* hc = s.h_cyc[slot];
+            const double span = batch_time(batch);
             cp_dirty = cpv;
-            KS_CHECK(read_ctl());
-            ms_bf_k += ev_ms(s.kev[0], s.kev[1]);
-            if (s.h_ctl->bf_done) {
+            if (cycle_log) {   // one line per batch: rounds so far, cycles so far, relaxations, time
+                std::vector<unsigned long long> hctr((size_t)CTR_SHARDS * NCTR);
+                KS_CHECK(hipMemcpy(hctr.data(), s.ctr.p, hctr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+                unsigned long long gsc = 0;
+                for (int i = 0; i < CTR_SHARDS; ++i) gsc += hctr[(size_t)i * NCTR + C_GUSCAN];
+                std::fprintf(stderr, "finish batch %d rounds %d worked %d cycles %d rejected %d relax %llu ms %.3f (searches %.3f)\n",
+                             batch, used, hc->bf_count, hc->cyc_done, hc->cyc_rej, gsc - gu_prev, span,
+                             (double)hc->srch_ticks / 1e5);
+                gu_prev = gsc;
+            }
+            if (hc->bf_done) {
                 ok = 1;
                 break;
             }
+            if (!more) break;   // the round cap: this was the last batch
+        }
+        if (nb > done_b) {   // the batch enqueued behind the converged one (its kernels exited at once)
+            KS_CHECK(hipEventSynchronize(end_ev(nb - 1)));
+            batch_time(nb - 1);
         }
         if (ok) hipLaunchKernelGGL(k_pr_apply, dim3(ngrid), dim3(BLK), 0, st, g, 1);
         KS_CHECK(hipEventRecord(s.ev[7], st));
@@ -4874,7 +4962,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int completed0 = 0;   // fs_completed at the phase's start of forward cycles
         // One cycle: [GU init (or continue the pending update)][kb BF rounds][max]
         // [apply][tail walks][gi sweeps][end: control block → pinned host memory].
-        // cev[0..1] bracket the Bellman-Ford rounds, cev[2..3] the sweeps.
+        // cev[0..1] bracket the Bellman-Ford rounds (the sweeps: device clock).
         auto enqueue = [&](int par) -> hipError_t {   // one cycle into slot par
             hipLaunchKernelGGL(k_gu_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, list);
             hipError_t e = hipEventRecord(s.cev[par][0], st);
@@ -4896,9 +4984,10 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 for (int wp = 1; wp < walk_passes; ++wp)
                     KS_HOT(cpv, k_augment, g.aug_k, WAVE, st, g, sseq, 0, wsl);
             }
-            if ((e = hipEventRecord(s.cev[par][2], st)) != hipSuccess) return e;
+            // (the sweeps are timed by the device clock — the first sweep's start to
+            // k_cycle_end's — not by HIP events: an event between two kernels costs a
+            // ~5.7 µs gap of its own, two per cycle; profiles/r06_*)
             for (int k = 0; k < gi; ++k) KS_HOT(cpv, k_sweep, wgrid, BLK, st, g, k, sseq + k);
-            if ((e = hipEventRecord(s.cev[par][3], st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_cycle_end, dim3(1), dim3(128), 0, st, g, s.d_cyc[par], 0);
             sseq += gi;
             return hipEventRecord(s.cdone[par], st);
@@ -4969,7 +5058,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_CHECK(hipEventSynchronize(s.cdone[cur]));
             const Ctl* hc = s.h_cyc[cur];
             sweep_kernels += gi;
-            const double t_bf = ev_ms(s.cev[cur][0], s.cev[cur][1]), t_sw = ev_ms(s.cev[cur][2], s.cev[cur][3]);
+            const double t_bf = ev_ms(s.cev[cur][0], s.cev[cur][1]);
+            const double t_sw = hc->t_end > hc->t_sw0 ? (double)(hc->t_end - hc->t_sw0) / 1e5 : 0.0;   // 100 MHz ticks
             ms_bf_k += t_bf;   // BF rounds only
             ms_sw_k += t_sw;   // sweeps only
             if (hc->infeasible) {
