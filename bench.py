@@ -78,10 +78,14 @@ def latency_stats(step_ms):
 
 
 def roofline_of(results, workload: str):
-    """HBM roofline of the dominant kernel (by event-timed device time) over the
-    timed steps: algorithmic bytes = SURVEY §8(d)'s 24 B per unit × the device
-    counters' units, divided by the HIP-event-timed duration of that kernel's
-    launches (each kind's span brackets exactly its own kernels, ks_result ABI 3).
+    """HBM roofline of the dominant kernel (by device time) over the timed steps:
+    algorithmic bytes = SURVEY §8(d)'s 24 B per unit × the device counters' units,
+    divided by the measured duration of that kernel's launches (ks_result ABI 3):
+    k_bf_round by HIP events on the engine's stream — each update's rounds
+    bracketed exactly, the finish's batches less their parent-graph searches
+    (timed by the device clock, s_memrealtime) — k_sweep by the device clock
+    (the first sweep's start to k_cycle_end's: an event between two kernels
+    would add a ~5.7 µs gap of its own), k_fs_round by HIP events.
     For k_bf_round the 44 B the relaxation actually reads is reported beside it;
     the forward search (k_fs_round) counts the residual out-arcs it examines.
     The cell solver (k_cell, one launch per solve) does all four kinds of work

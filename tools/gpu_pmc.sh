@@ -29,7 +29,7 @@ if [ "$PASSES" = all ]; then
     run_pass write "$ARGS" --pmc WRITE_SIZE
     run_pass atom "$ARGS" --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum
     run_pass ta "$ARGS" --pmc TA_FLAT_ATOMIC_WAVEFRONTS_sum
-    run_pass valu "$ARGS" --pmc SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU
+    run_pass valu "$ARGS" --pmc SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE
     python tools/pmc_per_kernel.py "$OUT/fetch" "$OUT/write" "$OUT/atom" "$OUT/ta" "$OUT/valu" > "$OUT/pmc_per_kernel.json"
 fi
 run_pass trace "$TARGS" --kernel-trace --stats

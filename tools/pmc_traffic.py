@@ -105,6 +105,14 @@ def main():
             rec["device_us_total"] = round(t["total_us"], 1)
             rec["trace_calls"] = t["calls"]
             rec["avg_launch_us"] = round(t["total_us"] / max(1, t["calls"]), 3)
+            if rec.get("valu"):
+                # CU utilisation: busy CU-cycles over all 256 CUs'
+                # cycles while the kernel runs, at the 2.4 GHz peak engine clock (a lower
+                # bound if the clock ran lower); GRBM_GUI_ACTIVE as measured, for reference
+                busy = rec["valu"]["busy_cu_cycles_per_launch"]
+                rec["valu"]["cu_busy_frac_at_peak_clock"] = round(busy / (256 * rec["avg_launch_us"] * 2400.0), 4)
+                if src.get("GRBM_GUI_ACTIVE"):
+                    rec["valu"]["grbm_gui_active_per_launch"] = round(src["GRBM_GUI_ACTIVE"] / nv, 1)
             # 64-bit atomics per second while the kernel runs: per-launch requests ÷ mean launch time
             rec["tcc_atomics_per_s"] = round(per["TCC_ATOMIC_sum"] / (rec["avg_launch_us"] / 1e6), 1)
         out["kernels"][name] = rec
