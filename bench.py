@@ -59,7 +59,10 @@ def pmc_file(workload: str):
 # times, its launch count and time fields, its algorithmic units
 KINDS = {
     "k_sweep": ("sweep_launches", "ms_sweep_kernels", ("arc_scans", "node_visits", "pushes")),
-    "k_bf_round": ("gu_launches", "ms_gu_kernels", ("gu_arc_scans",)),
+    # both hops of a round: the frontier's in-arcs and, for a task or PU whose distance
+    # just dropped, its own in-arcs in the same launch (ks_result.gu_leaf_scans, ABI 5;
+    # rounds 1-5 counted the first hop only — the line keeps that figure as *_first_hop)
+    "k_bf_round": ("gu_launches", "ms_gu_kernels", ("gu_arc_scans", "gu_leaf_scans")),
     "k_fs_round": ("fs_launches", "ms_fs_kernels", ("fs_arc_scans",)),
     "k_cell": (None, "ms_cell_kernel", ("arc_scans", "node_visits", "pushes", "gu_arc_scans")),
 }
@@ -116,11 +119,16 @@ def roofline_of(results, workload: str):
         a44 = B_RELAX * units / (ms / 1e3) / 1e9 if ms > 0 else 0.0
         line["achieved_44B"] = round(a44, 3)
         line["frac_44B"] = round(a44 / HBM_PEAK_GBS, 6)
+        first = sum(r.raw["gu_arc_scans"] for r in results if r.raw["solver"] == 0)
+        a1 = B_UNIT * first / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        line["units_per_launch_first_hop"] = round(first / max(1, n), 1)
+        line["achieved_first_hop"] = round(a1, 3)
+        line["frac_first_hop"] = round(a1 / HBM_PEAK_GBS, 6)
     # SURVEY §8(d) solve-level figure: B_work = 24 B × (arc scans + node visits + pushes)
     # over the whole solve time (and with the Bellman-Ford relaxations added), and the
     # single-pass floor B_pass = 2m·16 + n·24 for scale
     sw_units = sum(r.raw["arc_scans"] + r.raw["node_visits"] + r.raw["pushes"] for r in results)
-    bf_units = sum(r.raw["gu_arc_scans"] for r in results)
+    bf_units = sum(r.raw["gu_arc_scans"] + r.raw["gu_leaf_scans"] for r in results)
     t_solve = sum(r.raw["ms"]["total"] for r in results) / 1e3
     if t_solve > 0:
         nn, mm = results[-1].raw["n_nodes"], results[-1].raw["n_arcs"]

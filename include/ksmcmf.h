@@ -70,8 +70,8 @@ extern "C" {
                                   ks_opts), and three words of ks_result repurposed:
                                   cell_fallbacks and cycles_cancelled (two reserved words)
                                   and compact (the former _pad3); 5: ks_result.fb_resets
-                                  (the last reserved word) and ks_result.cycles_rejected;
-                                  ks_result grew to 352 B (3 reserved words).
+                                  (the last reserved word), ks_result.cycles_rejected and
+                                  gu_leaf_scans; ks_result grew to 352 B (2 reserved words).
                                   ks_opts (96 B) CHANGED SIZE in ABI 2 and ks_result in
                                   ABI 2, 3 and 5: a caller must check
                                   ks_abi_version() == KSMCMF_ABI_VERSION before ks_create. */
@@ -286,7 +286,11 @@ typedef struct ks_result {
                                   the union-of-cycles test found with other than one
                                   member pointing at them (engine), or leader walks
                                   that did not close a cycle (cell solver)            */
-    uint64_t reserved3[3];
+    uint64_t gu_leaf_scans;    /* ABI 5. Bellman-Ford rounds also relax the in-arcs of a task
+                                  or PU whose distance just dropped, in the same round
+                                  (two hops per round): those second-hop in-arc positions
+                                  examined (gu_arc_scans counts the first hop only)      */
+    uint64_t reserved3[2];
 } ks_result;
 
 /* Counters of the device-resident graph store (ks_get_store_stats). */

@@ -95,7 +95,7 @@ constexpr int SHARDS = 16;         // inbox shards per heavy hub
 constexpr int MAXB = 64;           // max sweeps per cycle
 constexpr int HUB_LDS = 16;        // hubs whose Bellman-Ford minima are reduced in LDS
 constexpr int CYC_SLOTS = 2;       // control snapshots / timing events rotate over two cycles
-constexpr int NCTR = 9;
+constexpr int NCTR = 10;
 constexpr int CTR_SHARDS = 64;
 constexpr long long INF64 = 0x3fffffffffffffffLL;
 constexpr long long LEN_CAP = 1LL << 40;   // global-update arc length clamp
@@ -103,7 +103,7 @@ constexpr double kSolveWallLimitS = 120.0; // host-side guard against a non-conv
 constexpr double kCellLimitS = 20.0;       // the cell solver's in-kernel wall-clock limit (every workgroup exits)
 
 enum { C_SCAN = 0, C_VISIT = 1, C_PUSH = 2, C_RELABEL = 3, C_GUSCAN = 4, C_BFROUND = 5, C_AUGWALK = 6, C_AUGHOP = 7,
-       C_FSSCAN = 8 };
+       C_FSSCAN = 8, C_GULEAF = 9 };
 constexpr int AUG_KMAX = 4096;     // most excess nodes a tail's walkers start from (ks_opts.tail_nodes)
 constexpr int BX_CAP = 64;         // global updates with at most this many excess nodes are bounded
 // Forward tail update: a node's search key (in its record's dist slot) packs the
@@ -1454,7 +1454,9 @@ __device__ __forceinline__ bool offer(const DG& g, const Front& nf, int u, long 
 // its distance dropped to du: a second hop inside the same round.
 template <int PR, bool CP>
 __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u, long long du, long long pu,
-                                            int b0, int b1, long long eps, long long B, long long* hub_min, int& out) {
+                                            int b0, int b1, long long eps, long long B, long long* hub_min, int& out,
+                                            long long& lscan) {
+    lscan += b1 - b0;   // the second hop's in-arc positions examined (ks_result.gu_leaf_scans)
     // the records of all (≤ 8) arcs issued together; usually one in-arc carries
     // flow (a task's assignment), so the dependent loads follow for it alone
     unsigned live = 0;
@@ -1509,7 +1511,7 @@ __device__ __forceinline__ void expand_leaf(const DG& g, const Front& nf, int u,
 // cost −cost(a). Loads are issued before the residual test (short chain).
 template <int PR, bool CP>
 __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int v, int a, long long dv, long long pv,
-                                         long long eps, long long B, long long* hub_min, int& out) {
+                                         long long eps, long long B, long long* hub_min, int& out, long long& lscan) {
     const Pos q = PL<CP>::ld_nr(g, a);
     const long long rin = q.ucap - q.rcap;
     // an arc that cannot relax reads node 0's (hot) record instead of its head's
@@ -1526,7 +1528,7 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int v, in
     const long long cand = dv + arc_len<PR>(pu, ca, pv, eps);   // (dv decoded: a distance in every mode)
     if (!offer<PR>(g, nf, u, PR == 2 ? pk(cand, a) : cand, du, B, hub_min, out)) return;
     if (leaf) {
-        expand_leaf<PR, CP>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out);   // tasks, PUs: two hops per round
+        expand_leaf<PR, CP>(g, nf, u, cand, pu, b0, b1, eps, B, hub_min, out, lscan);   // tasks, PUs: two hops per round
     } else {
         nf.flag[u] = 1;
         out = 1;
@@ -1535,7 +1537,7 @@ __device__ __forceinline__ void relax_in(const DG& g, const Front& nf, int v, in
 
 template <int G, int PR, bool CP>
 __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v, long long dv, long long pv, int b0,
-                                             int en, long long eps, long long B, long long* hub_min, int& out, long long& scans) {
+                                             int en, long long eps, long long B, long long* hub_min, int& out, long long& scans, long long& lscan) {
     const int lig = lane_id() & (G - 1);
     const bool act = v >= 0 && (PR || dv < INF64);
     if (!act) en = b0;
@@ -1543,7 +1545,7 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out, lscan);
             scans++;
         }
     }
@@ -1552,7 +1554,7 @@ __device__ __forceinline__ void bf_group_pre(const DG& g, const Front& nf, int v
 // Sparse Bellman-Ford pass over window w of class C (mask from window_mask).
 template <int C, int PR, bool CP>
 __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsigned long long mask, const WinFlag& f,
-                                       long long eps, long long B, long long* hub_min, int& out, long long& scans) {
+                                       long long eps, long long B, long long* hub_min, int& out, long long& scans, long long& lscan) {
     constexpr int G = class_lanes(C);
     constexpr int PER = 64 / G;
     constexpr int WS = win_slots(C);
@@ -1566,7 +1568,7 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
         int b0 = 0, en = 0;
         window_node(f, v, base, d, pv, b0, en);
         if (v < 0) d = INF64;
-        bf_group_pre<G, PR, CP>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans);
+        bf_group_pre<G, PR, CP>(g, N, v, d, pv, b0, en, eps, B, hub_min, out, scans, lscan);
         for (int j = 0; j < PER; ++j) mask &= mask - 1;
     }
 }
@@ -1574,19 +1576,19 @@ __device__ __forceinline__ void bf_win(const DG& g, const Front& N, int w, unsig
 // One 64-arc chunk of a chunked-class node (its flag already tested).
 template <int PR, bool CP>
 __device__ __forceinline__ void bf_chunk(const DG& g, const Front& N, const CItem& ci, long long eps,
-                                         long long B, long long* hub_min, int& out, long long& scans) {
+                                         long long B, long long* hub_min, int& out, long long& scans, long long& lscan) {
     const long long dv = atom_load(&g.dist[ni(ci.node)]);
     if (!PR && dv >= INF64) return;
     const int a = ci.begin + lane_id();
     if (a < ci.end) {
-        relax_in<PR, CP>(g, N, ci.node, a, dkey<PR>(dv), g.p0[ni(ci.node)], eps, B, hub_min, out);
+        relax_in<PR, CP>(g, N, ci.node, a, dkey<PR>(dv), g.p0[ni(ci.node)], eps, B, hub_min, out, lscan);
         scans++;
     }
 }
 
 template <int G, int PR, bool CP>
 __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, long long eps, long long B, long long* hub_min,
-                                         int& out, long long& scans) {
+                                         int& out, long long& scans, long long& lscan) {
     const int lig = lane_id() & (G - 1);
     long long dv = INF64;
     if (v >= 0) dv = atom_load(&g.dist[ni(v)]);
@@ -1601,7 +1603,7 @@ __device__ __forceinline__ void bf_group(const DG& g, const Front& nf, int v, lo
     for (int it = 0; it < iters; ++it) {
         const int a = b0 + it * G + lig;
         if (a < en) {
-            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
+            relax_in<PR, CP>(g, nf, v, a, dkey<PR>(dv), pv, eps, B, hub_min, out, lscan);
             scans++;
         }
     }
@@ -1635,7 +1637,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
     // tentative distance are dropped (that bound only falls, so a stale copy is safe)
     const long long B = (!PR && g.bound) ? atom_load(&g.ctl->bf_bound) : INF64;
     int out = 0;
-    long long scans = 0;
+    long long scans = 0, lscan = 0;
     // Hub chunks are split over HSPLIT workgroups: a relaxation is a dependent
     // chain (arc, tail record, leaf expansion, atomic), and a thread that runs
     // several of them in a row made the hub the last block of its round.
@@ -1654,7 +1656,7 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
                 for (int k = 0; k < BF_PER_T; ++k) {
                     const int a = it.begin + sub * (CHUNK / HSPLIT) + threadIdx.x * BF_PER_T + k;
                     if (a < it.end) {
-                        relax_in<PR, CP>(g, N, it.node, a, dkey<PR>(dv), pv, eps, B, hub_min, out);
+                        relax_in<PR, CP>(g, N, it.node, a, dkey<PR>(dv), pv, eps, B, hub_min, out, lscan);
                         scans++;
                     }
                 }
@@ -1667,11 +1669,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             // the update already converged
         } else if (w < g.wbeg[CCLS]) {
             const Scan sc{F.flag, 1};
-#define KS_BF_CALL(C) bf_group<G_, PR, CP>(g, N, v, eps, B, hub_min, out, scans)
+#define KS_BF_CALL(C) bf_group<G_, PR, CP>(g, N, v, eps, B, hub_min, out, scans, lscan)
             KS_BY_CLASS(w, sc, KS_BF_CALL)
 #undef KS_BF_CALL
         } else if (w - g.wbeg[CCLS] < g.ncitems) {
-            bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
+            bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans, lscan);
         }
     } else {
         const int tw = ((int)gridDim.x - nhb) * WPB;
@@ -1703,15 +1705,15 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
             if (!mk[j]) continue;
             const int w = w0 + j * tw;
             if (w >= g.wbeg[CCLS]) {
-                bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans);
+                bf_chunk<PR, CP>(g, N, g.citems[w - g.wbeg[CCLS]], eps, B, hub_min, out, scans, lscan);
                 continue;
             }
             switch (class_of_window(g, w)) {
-                case 0: bf_win<0, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 1: bf_win<1, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 2: bf_win<2, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                case 3: bf_win<3, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
-                default: bf_win<4, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans); break;
+                case 0: bf_win<0, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans, lscan); break;
+                case 1: bf_win<1, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans, lscan); break;
+                case 2: bf_win<2, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans, lscan); break;
+                case 3: bf_win<3, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans, lscan); break;
+                default: bf_win<4, PR, CP>(g, N, w, mk[j], wf[j], eps, B, hub_min, out, scans, lscan); break;
             }
         }
     }
@@ -1752,9 +1754,11 @@ __global__ __launch_bounds__(BLK) void k_bf_round(DG g, int seq, int dense_arg) 
         }
     }
     scans = wave_sum(scans);
-    if (lane_id() == 0 && scans) {
+    lscan = wave_sum(lscan);
+    if (lane_id() == 0 && (scans | lscan)) {
         const int sh = ((blockIdx.x * WPB) + (threadIdx.x >> 6)) & (CTR_SHARDS - 1);
-        atomicAdd(g.ctr + sh * NCTR + C_GUSCAN, (unsigned long long)scans);
+        if (scans) atomicAdd(g.ctr + sh * NCTR + C_GUSCAN, (unsigned long long)scans);
+        if (lscan) atomicAdd(g.ctr + sh * NCTR + C_GULEAF, (unsigned long long)lscan);
     }
 }
 
@@ -1874,6 +1878,21 @@ __global__ void k_cycle_end(DG g, Ctl* host, int fwd) {
 
 // max finite distance (only once the update converged); cleans the sweep
 // frontiers and flags the apply step and the sweeps write.
+constexpr int SET_FWD = 1;   // k_set_eps: no forward search pending, its counters zeroed
+constexpr int SET_CYC = 2;   //            the finish's cycle counters zeroed
+__global__ void k_set_eps(DG g, long long eps, int flags) {
+    g.ctl->eps = eps;
+    if (flags & SET_FWD) {
+        g.ctl->fs_pending = 0;
+        g.ctl->fs_cnt[0] = g.ctl->fs_cnt[1] = g.ctl->fs_cnt[2] = 0;
+        g.ctl->fs_completed = 0;
+    }
+    if (flags & SET_CYC) {
+        g.ctl->cyc_done = 0;
+        g.ctl->cyc_rej = 0;
+    }
+}
+
 // The finish's batch end: closes the running search's time and copies the control
 // block into pinned host memory (no copy-engine transfer: that drains the queue).
 __global__ void k_prc_snap(DG g, Ctl* host) {
@@ -4703,9 +4722,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         if (e != hipSuccess) return e;
         return hipStreamSynchronize(st);
     };
-    auto set_eps = [&](long long e) -> hipError_t {
-        s.h_scr[0] = e;
-        return hipMemcpyAsync(&s.ctl.p->eps, &s.h_scr[0], sizeof(long long), hipMemcpyHostToDevice, st);
+    // ε (and, by flags, the control words a phase or the finish starts from) set by a
+    // one-thread kernel: a host-to-device copy is a copy kernel behind a staging gap,
+    // and each memset another launch
+    auto set_eps = [&](long long e, int flags = 0) -> hipError_t {
+        hipLaunchKernelGGL(k_set_eps, dim3(1), dim3(1), 0, st, g, e, flags);
+        return hipGetLastError();
     };
     // mode 0: global update; 1: price refinement; 2: refinement with parents (cycle cancelling)
     auto bf_rounds = [&](int mode, int k, bool first_dense) {
@@ -4774,8 +4796,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         int* indeg = gbad + nn;   // members of its group pointing at a node
         long long* gsum = s.cyc64.p;
         long long* gcap = gsum + nn;
-        KS_CHECK(set_eps(1));
-        KS_CHECK(hipMemsetAsync(&s.ctl.p->cyc_done, 0, 2 * sizeof(int), st));   // cyc_done, cyc_rej
+        KS_CHECK(set_eps(1, SET_CYC));   // and cyc_done, cyc_rej zeroed
         hipLaunchKernelGGL(k_pr_init, dim3(ngrid), dim3(BLK), 0, st, g, bseq, 2);
         const int* done = &s.ctl.p->bf_done;
         // the parent graph: pointer doubling over CYC_WALK steps, cycles grouped by
@@ -4920,8 +4941,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     // rounds, 0.07–0.11 of the supply, vs ≥ 1.9 for cold configs 2 and 3)
     auto run_phase = [&](long long eps_ph, long long sat_thr, bool may_end_early, int walk_sl,
                          int* prc_early = nullptr) -> int {
-        KS_CHECK(set_eps(eps_ph));
         KS_CHECK(hipEventRecord(s.ev[2], st));
+        KS_CHECK(set_eps(eps_ph, use_fwd ? SET_FWD : 0));   // a phase never continues another phase's forward search
         KS_HOT(cpv, k_saturate, fgrid, BLK, st, g, sat_thr);
         cp_dirty = cpv;
         KS_CHECK(hipEventRecord(s.ev[3], st));
@@ -4995,12 +5016,12 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         // Cycles run one at a time (enqueueing the next one before reading this
         // one's control block was measured slower: the speculative launches cost
         // more GPU time than the host's decision gap).
-        if (use_fwd) {   // a phase never continues another phase's forward search
-            KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_pending, 0, sizeof(int), st));
-            KS_CHECK(hipMemsetAsync(s.ctl.p->fs_cnt, 0, sizeof(s.ctl.p->fs_cnt), st));
-            KS_CHECK(hipMemsetAsync(&s.ctl.p->fs_completed, 0, sizeof(int), st));
-        }
         int cur = 0;
+        int bf_pend = -1;   // a cycle whose Bellman-Ford event span is not read yet
+        auto flush_bf = [&]() {
+            if (bf_pend >= 0) ms_bf_k += ev_ms(s.cev[bf_pend][0], s.cev[bf_pend][1]);
+            bf_pend = -1;
+        };
         for (;;) {
             if (fwd) {
                 KS_CHECK(enqueue_fwd(cur, nupd));
@@ -5054,13 +5075,20 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
                 }
                 continue;
             }
+            if (bf_pend == cur) flush_bf();   // (the slot's events are about to be recorded again)
             KS_CHECK(enqueue(cur));
+            flush_bf();   // the previous cycle's event time, read while this one runs
             KS_CHECK(hipEventSynchronize(s.cdone[cur]));
             const Ctl* hc = s.h_cyc[cur];
             sweep_kernels += gi;
-            const double t_bf = ev_ms(s.cev[cur][0], s.cev[cur][1]);
+            double t_bf = 0;
+            if (cycle_log) {
+                t_bf = ev_ms(s.cev[cur][0], s.cev[cur][1]);
+                ms_bf_k += t_bf;   // BF rounds only
+            } else {
+                bf_pend = cur;     // read after the next cycle is enqueued (off the host's critical path)
+            }
             const double t_sw = hc->t_end > hc->t_sw0 ? (double)(hc->t_end - hc->t_sw0) / 1e5 : 0.0;   // 100 MHz ticks
-            ms_bf_k += t_bf;   // BF rounds only
             ms_sw_k += t_sw;   // sweeps only
             if (hc->infeasible) {
                 rc = KS_E_INFEASIBLE;
@@ -5132,6 +5160,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             }
             cur ^= 1;
         }
+        flush_bf();
         KS_CHECK(hipEventRecord(s.ev[5], st));
         KS_CHECK(hipEventSynchronize(s.ev[5]));
         ms_sat += ev_ms(s.ev[2], s.ev[3]);
@@ -5550,6 +5579,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
     res.ms_phase[4] = ev_ms(s.ev[6], s.ev[7]);
     res.ms_phase[5] = 1e3 * wall_s();
     res.gu_arc_scans = tc[C_GUSCAN];
+    res.gu_leaf_scans = tc[C_GULEAF];
     res.fs_arc_scans = tc[C_FSSCAN];
     res.sweep_launches = sweep_kernels;
     res.ms_sweep_kernels = ms_sw_k;

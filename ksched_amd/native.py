@@ -70,7 +70,7 @@ class KsResult(C.Structure):
                 ("cells", C.c_int32), ("compact", C.c_int32), ("ms_cell_kernel", C.c_double),
                 ("cell_ticks_max", C.c_uint64), ("cell_ticks_sum", C.c_uint64), ("fs_arc_scans", C.c_uint64),
                 ("cell_fallbacks", C.c_uint64), ("cycles_cancelled", C.c_uint64), ("fb_resets", C.c_uint64),
-                ("cycles_rejected", C.c_uint64), ("reserved3", C.c_uint64 * 3)]
+                ("cycles_rejected", C.c_uint64), ("gu_leaf_scans", C.c_uint64), ("reserved3", C.c_uint64 * 2)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("ms_phase", "reserved3")}

@@ -63,7 +63,7 @@ int main(void) {
   P(ks_delta, cost); P(ks_delta, old_cost); P(ks_delta, excess);
   P(ks_result, status); P(ks_result, sweeps); P(ks_result, ms_phase); P(ks_result, n_nodes);
   P(ks_result, ms_gu_kernels); P(ks_result, rebuilt); P(ks_result, recoveries); P(ks_result, cell_fallbacks);
-  P(ks_result, cycles_cancelled); P(ks_result, fb_resets); P(ks_result, compact); P(ks_result, cycles_rejected);
+  P(ks_result, cycles_cancelled); P(ks_result, fb_resets); P(ks_result, compact); P(ks_result, cycles_rejected); P(ks_result, gu_leaf_scans);
   P(ks_opts, warm_start); P(ks_opts, walk_slack); P(ks_opts, fault_inject); P(ks_opts, walk_passes); P(ks_opts, tail_nodes); P(ks_opts, bf_bound); P(ks_opts, fwd_nodes); P(ks_opts, cell_nodes); P(ks_opts, warm_shift); P(ks_opts, warm_canon); P(ks_opts, compact_pos);
   P(ks_store_stats, superseded); P(ks_store_stats, residual_slots);
   P(ks_flow, flow);
@@ -96,7 +96,7 @@ def test_struct_layouts_match_bindings(tmp_path):
             if key in out:
                 assert dt.fields[f][1] == out[key], key
     for f in ("status", "sweeps", "ms_phase", "n_nodes", "ms_gu_kernels", "rebuilt", "recoveries", "cell_fallbacks",
-              "cycles_cancelled", "fb_resets", "compact", "cycles_rejected"):
+              "cycles_cancelled", "fb_resets", "compact", "cycles_rejected", "gu_leaf_scans"):
         assert getattr(native.KsResult, f).offset == out[f"ks_result.{f}"], f
     for f in ("warm_start", "walk_slack", "fault_inject", "walk_passes", "tail_nodes", "bf_bound", "fwd_nodes",
               "cell_nodes", "warm_shift", "warm_canon", "compact_pos"):

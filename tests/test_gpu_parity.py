@@ -518,3 +518,21 @@ def test_cycle_search_without_the_check_fails_loudly():
                 continue
             assert (r.cost, r.flow) == (cost, flow)
     assert failed > 0, "no chain was pushed along: the unchecked search never met the bad case"
+
+
+def test_kind_timing_and_counters():
+    """The per-kind device times the bench's roofline divides by (ks_result ABI 3/5):
+    the Bellman-Ford rounds by HIP events less the finish's searches (device
+    clock), the sweeps by the device clock — each positive and together within the
+    solve's own time; and both hops of a Bellman-Ford round counted (the second,
+    a task's or PU's own in-arcs in the same launch: gu_leaf_scans)."""
+    g = gen.quincy(10_000, 1_000, 25, 100, 2)
+    with native.Context(0, cell_nodes=-1) as c:
+        c.load_graph(g)
+        for _ in range(2):
+            r = c.solve()
+            raw = r.raw
+            assert raw["ms_gu_kernels"] > 0 and raw["ms_sweep_kernels"] > 0
+            assert raw["ms_gu_kernels"] + raw["ms_sweep_kernels"] < raw["ms"]["total"]
+            assert raw["gu_arc_scans"] > 0 and raw["gu_leaf_scans"] > 0
+            assert raw["gu_launches"] >= raw["gu_iterations"] > 0
