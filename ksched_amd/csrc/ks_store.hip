@@ -65,11 +65,31 @@ __device__ int h_find(const StoreDev& d, unsigned long long k) {
     return -1;
 }
 
-__device__ __forceinline__ void h_tomb(const StoreDev& d, int e) {
-    if (e < 0) return;
+// Wave-aggregated counter updates and slot allocation. A round's delta stream
+// deletes and inserts tens of thousands of arcs (config 4: ~25k of each), and
+// one atomic per record on the same control word serialises at the memory-side
+// atomic unit (~10 ns each: k_arc_deletes took ~0.8 ms per config-4 round). The
+// lanes of a wave that are active at the call combine into one atomic.
+__device__ __forceinline__ void wave_count(int* ctr, bool pred, int sign = 1) {
+    const unsigned long long m = __ballot(pred);
+    if (m && (int)__lane_id() == __ffsll((long long)m) - 1) atomicAdd(ctr, sign * __popcll(m));
+}
+// pred lanes take consecutive values base, base + 1, … of *top (one atomicAdd of the count)
+__device__ __forceinline__ int wave_take(int* top, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (!m) return -1;
+    const int lead = __ffsll((long long)m) - 1;
+    int base = 0;
+    if ((int)__lane_id() == lead) base = atomicAdd(top, __popcll(m));
+    base = __shfl(base, lead);
+    return pred ? base + __popcll(m & ((1ULL << __lane_id()) - 1)) : -1;
+}
+
+__device__ __forceinline__ int h_tomb(const StoreDev& d, int e) {   // 1 when the entry became a tombstone
+    if (e < 0) return 0;
     const unsigned long long was = atomicExch(&d.hkey[e], HKEY_TOMB);
     d.hval[e] = -1;
-    if (was != HKEY_TOMB) atomicAdd(&d.ctl->tombs, 1);
+    return was != HKEY_TOMB;
 }
 
 __device__ __forceinline__ void inert(const StoreDev& d, int p, int owner) {
@@ -101,13 +121,17 @@ __device__ void kill_positions(const StoreDev& d, int s) {
     inert(d, q, xd);
 }
 
-__device__ __forceinline__ void free_slot(const StoreDev& d, int s) {
-    d.a_alive[s] = 0;
-    d.fwd[s] = -1;
-    const int t = atomicAdd(&d.ctl->free_top, 1);
-    d.free_stack[t] = s;
-    atomicSub(&d.ctl->live, 1);
-    atomicAdd(&d.ctl->killed, 1);
+// Free arc slot s on the lanes where fr is set (every active lane of the wave
+// calls it: the stack slots and the counters are taken once per wave).
+__device__ __forceinline__ void free_slots(const StoreDev& d, int s, bool fr) {
+    if (fr) {
+        d.a_alive[s] = 0;
+        d.fwd[s] = -1;
+    }
+    const int t = wave_take(&d.ctl->free_top, fr);
+    if (fr) d.free_stack[t] = s;
+    wave_count(&d.ctl->live, fr, -1);
+    wave_count(&d.ctl->killed, fr);
 }
 
 // A free (inert, ent = −1) position in node x's segment, claimed for the entry
@@ -165,16 +189,19 @@ __global__ void k_hash_records(StoreDev d, const ks_delta* __restrict__ r, int k
 
 __global__ void k_kill_scan(StoreDev d, int hi) {
     for (int s = blockIdx.x * SBLK + threadIdx.x; s < hi; s += gridDim.x * SBLK) {
-        if (!d.a_alive[s]) continue;
-        const int lr = max(d.n_lastrm[d.a_src[s]], d.n_lastrm[d.a_dst[s]]);
-        if (lr < 0) continue;
-        const int e = h_find(d, arc_hkey((long long)d.a_src[s] + 1, (long long)d.a_dst[s] + 1));
-        const int last = e >= 0 ? d.hlast[e] : -1;
-        kill_positions(d, s);
-        if (last < lr) {          // no record after the removal re-creates it
-            free_slot(d, s);
-            h_tomb(d, e);
-        }                         // else: alive with fwd = −1, re-inserted by k_arc_upserts
+        bool fr = false;
+        int e = -1;
+        if (d.a_alive[s]) {
+            const int lr = max(d.n_lastrm[d.a_src[s]], d.n_lastrm[d.a_dst[s]]);
+            if (lr >= 0) {
+                e = h_find(d, arc_hkey((long long)d.a_src[s] + 1, (long long)d.a_dst[s] + 1));
+                const int last = e >= 0 ? d.hlast[e] : -1;
+                kill_positions(d, s);
+                fr = last < lr;   // no record after the removal re-creates it; else alive with
+            }                     // fwd = −1, re-inserted by k_arc_upserts
+        }
+        free_slots(d, s, fr);
+        wave_count(&d.ctl->tombs, fr && h_tomb(d, e));
     }
 }
 
@@ -214,113 +241,136 @@ __device__ __forceinline__ bool killed_later(const StoreDev& d, const ks_delta& 
 __global__ void k_arc_deletes(StoreDev d, const ks_delta* __restrict__ r, int k, const int* __restrict__ rec_ent) {
     for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
         const int e = rec_ent[i];
-        if (e < 0) continue;
-        if (d.hlast[e] != i) {
-            atomicAdd(&d.ctl->superseded, 1);
-            continue;
+        bool sup = false, fr = false, tomb = false;
+        int s = -1;
+        if (e >= 0) {
+            sup = d.hlast[e] != i;
+            if (!sup) {
+                const ks_delta x = r[i];
+                const bool del = x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0;
+                if (del || killed_later(d, x, i)) {
+                    s = d.hval[e];
+                    fr = s >= 0 && d.a_alive[s];   // (a slot killed by k_kill_scan is already free)
+                    if (fr) kill_positions(d, s);
+                    tomb = h_tomb(d, e);
+                }
+            }
         }
-        const ks_delta x = r[i];
-        const bool del = x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0;
-        const bool dead = killed_later(d, x, i);
-        if (!del && !dead) continue;
-        const int s = d.hval[e];
-        if (s >= 0 && d.a_alive[s]) {   // (a slot killed by k_kill_scan is already free)
-            kill_positions(d, s);
-            free_slot(d, s);
-        }
-        h_tomb(d, e);
+        wave_count(&d.ctl->superseded, sup);
+        free_slots(d, s, fr);
+        wave_count(&d.ctl->tombs, tomb);
     }
+}
+
+// Record x applied to arc slot s: 1 edited in place, 2 inserted into the CSR, 0 otherwise.
+__device__ int upsert_slot(const StoreDev& d, const ks_delta& x, int s) {
+    const int sl = (int)x.src - 1, dl = (int)x.dst - 1;
+    const long long low = (long long)x.low, cap = (long long)x.cap, u = cap - low;
+    const long long low_old = d.a_low[s], cost_old = d.a_cost[s];
+    d.a_src[s] = sl;
+    d.a_dst[s] = dl;
+    d.a_low[s] = low;
+    d.a_cap[s] = cap;
+    d.a_cost[s] = x.cost;
+    d.a_type[s] = (unsigned char)(x.type < 0 ? 0 : (x.type > 255 ? 255 : x.type));
+    if (!d.csr_valid) return 0;
+    const int xs = perm_of(d, sl), xd = perm_of(d, dl);
+    if (xs < 0 || xd < 0) {
+        d.ctl->overflow |= 2;
+        return 0;
+    }
+    const int p0 = d.fwd[s];
+    if (p0 >= 0) {                  // in place: same endpoints, new bounds / cost
+        const int q0 = d.pos[p0].rev;
+        const long long f = d.pos[q0].rcap;
+        const long long fn = f < 0 ? 0 : (f > u ? u : f);
+        d.pos[p0].rcap = u - fn;
+        d.pos[q0].rcap = fn;
+        d.pos[p0].ucap = u;
+        d.pos[q0].ucap = u;
+        d.pos[p0].cost = x.cost * d.mult;
+        d.pos[q0].cost = -x.cost * d.mult;
+        const long long back = (f - fn) - (low - low_old);   // units returned to the tail
+        if (back) {
+            atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)back);
+            atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)(-back));
+        }
+        // a cost rise on an arc that keeps its flow (ksched's ageing of the
+        // arcs to the unscheduled aggregators, graph_manager.go:462-475): the
+        // warm start lowers the tail's price by it, so the arc keeps its reduced
+        // cost and only the tail's other arcs lose that much slack
+        if (fn > 0 && x.cost > cost_old)
+            atomicMax(&d.n_cshift[sl], (unsigned long long)(x.cost - cost_old));
+        return 1;
+    }
+    // both endpoints claim (so a full segment is flagged at each end at once); a
+    // claim that cannot be paired is given back
+    const int p = claim_pos(d, xs, 2 * s), q = claim_pos(d, xd, 2 * s + 1);
+    if (p < 0 || q < 0) {
+        d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
+        if (p < 0) d.n_grow[sl] = 1;
+        if (q < 0) d.n_grow[dl] = 1;
+        if (p >= 0) atomicExch(&d.ent[p], -1);
+        if (q >= 0) atomicExch(&d.ent[q], -1);
+        return 0;
+    }
+    d.pos[p].head = xd;
+    d.pos[p].rev = q;
+    d.pos[p].rcap = u;
+    d.pos[p].ucap = u;
+    d.pos[p].cost = x.cost * d.mult;
+    d.ent[p] = 2 * s;
+    d.pos[q].head = xs;
+    d.pos[q].rev = p;
+    d.pos[q].rcap = 0;
+    d.pos[q].ucap = u;
+    d.pos[q].cost = -x.cost * d.mult;
+    d.ent[q] = 2 * s + 1;
+    d.fwd[s] = p;
+    if (low) {                      // lower-bound transform
+        atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)(-low));
+        atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)low);
+    }
+    return 2;
 }
 
 __global__ void k_arc_upserts(StoreDev d, const ks_delta* __restrict__ r, int k, const int* __restrict__ rec_ent) {
     for (int i = blockIdx.x * SBLK + threadIdx.x; i < k; i += gridDim.x * SBLK) {
         const int e = rec_ent[i];
-        if (e < 0 || d.hlast[e] != i) continue;
-        const ks_delta x = r[i];
-        if ((x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0) || killed_later(d, x, i)) continue;
-        int s = d.hval[e];
-        if (s < 0) {                    // a new arc: a free slot, else a fresh one
-            const int t = atomicSub(&d.ctl->free_top, 1) - 1;
-            if (t >= 0) s = d.free_stack[t];
-            else s = atomicAdd(&d.ctl->hi, 1);
-            if (s >= d.acap) {          // the host sizes the table first; never expected
-                d.ctl->overflow |= 8;
-                continue;
-            }
+        bool up = e >= 0 && d.hlast[e] == i;
+        ks_delta x{};
+        if (up) {
+            x = r[i];
+            up = !((x.kind == KS_UPDATE_ARC && x.low == 0 && x.cap == 0) || killed_later(d, x, i));
+        }
+        int s = up ? d.hval[e] : -1;
+        // a new arc: a free slot, else a fresh one. The free-slot stack is popped and
+        // fresh slots are handed out once per wave; the stack top may run below zero
+        // (those lanes take fresh slots; k_finish resets it), as with one pop per lane.
+        const bool fresh = up && s < 0;
+        const unsigned long long fm = __ballot(fresh);
+        if (fm) {
+            const int lead = __ffsll((long long)fm) - 1;
+            int top = 0;
+            if ((int)__lane_id() == lead) top = atomicSub(&d.ctl->free_top, __popcll(fm));
+            top = __shfl(top, lead);
+            const int t = top - 1 - __popcll(fm & ((1ULL << __lane_id()) - 1));   // this lane's stack entry
+            const int h = wave_take(&d.ctl->hi, fresh && t < 0);
+            if (fresh) s = t >= 0 ? d.free_stack[t] : h;
+        }
+        int res = 0;
+        if (fresh && s >= d.acap) {   // the host sizes the table first; never expected
+            d.ctl->overflow |= 8;
+            up = false;
+        } else if (fresh) {
             d.hval[e] = s;
             d.a_alive[s] = 1;
             d.fwd[s] = -1;
-            atomicAdd(&d.ctl->live, 1);
         }
-        const int sl = (int)x.src - 1, dl = (int)x.dst - 1;
-        const long long low = (long long)x.low, cap = (long long)x.cap, u = cap - low;
-        const long long low_old = d.a_low[s], cost_old = d.a_cost[s];
-        d.a_src[s] = sl;
-        d.a_dst[s] = dl;
-        d.a_low[s] = low;
-        d.a_cap[s] = cap;
-        d.a_cost[s] = x.cost;
-        d.a_type[s] = (unsigned char)(x.type < 0 ? 0 : (x.type > 255 ? 255 : x.type));
-        if (!d.csr_valid) continue;
-        const int xs = perm_of(d, sl), xd = perm_of(d, dl);
-        if (xs < 0 || xd < 0) {
-            d.ctl->overflow |= 2;
-            continue;
-        }
-        const int p0 = d.fwd[s];
-        if (p0 >= 0) {                  // in place: same endpoints, new bounds / cost
-            const int q0 = d.pos[p0].rev;
-            const long long f = d.pos[q0].rcap;
-            const long long fn = f < 0 ? 0 : (f > u ? u : f);
-            d.pos[p0].rcap = u - fn;
-            d.pos[q0].rcap = fn;
-            d.pos[p0].ucap = u;
-            d.pos[q0].ucap = u;
-            d.pos[p0].cost = x.cost * d.mult;
-            d.pos[q0].cost = -x.cost * d.mult;
-            const long long back = (f - fn) - (low - low_old);   // units returned to the tail
-            if (back) {
-                atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)back);
-                atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)(-back));
-            }
-            // a cost rise on an arc that keeps its flow (ksched's ageing of the
-            // arcs to the unscheduled aggregators, graph_manager.go:462-475): the
-            // warm start lowers the tail's price by it, so the arc keeps its reduced
-            // cost and only the tail's other arcs lose that much slack
-            if (fn > 0 && x.cost > cost_old)
-                atomicMax(&d.n_cshift[sl], (unsigned long long)(x.cost - cost_old));
-            atomicAdd(&d.ctl->updated, 1);
-            continue;
-        }
-        // both endpoints claim (so a full segment is flagged at each end at once); a
-        // claim that cannot be paired is given back
-        const int p = claim_pos(d, xs, 2 * s), q = claim_pos(d, xd, 2 * s + 1);
-        if (p < 0 || q < 0) {
-            d.ctl->overflow |= 1;       // a full segment: the host rebuilds from the table
-            if (p < 0) d.n_grow[sl] = 1;
-            if (q < 0) d.n_grow[dl] = 1;
-            if (p >= 0) atomicExch(&d.ent[p], -1);
-            if (q >= 0) atomicExch(&d.ent[q], -1);
-            continue;
-        }
-        d.pos[p].head = xd;
-        d.pos[p].rev = q;
-        d.pos[p].rcap = u;
-        d.pos[p].ucap = u;
-        d.pos[p].cost = x.cost * d.mult;
-        d.ent[p] = 2 * s;
-        d.pos[q].head = xs;
-        d.pos[q].rev = p;
-        d.pos[q].rcap = 0;
-        d.pos[q].ucap = u;
-        d.pos[q].cost = -x.cost * d.mult;
-        d.ent[q] = 2 * s + 1;
-        d.fwd[s] = p;
-        if (low) {                      // lower-bound transform
-            atomicAdd((unsigned long long*)&d.excess[xs], (unsigned long long)(-low));
-            atomicAdd((unsigned long long*)&d.excess[xd], (unsigned long long)low);
-        }
-        atomicAdd(&d.ctl->inserted, 1);
+        if (up) res = upsert_slot(d, x, s);
+        wave_count(&d.ctl->live, fresh && up);
+        wave_count(&d.ctl->updated, res == 1);
+        wave_count(&d.ctl->inserted, res == 2);
     }
 }
 
