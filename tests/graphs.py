@@ -190,3 +190,63 @@ def same_graph(ctx, g):
     assert dev == want
     live = np.nonzero(g.ntype != 0)[0] + 1
     assert set(live.tolist()) <= set(nodes["id"].tolist())
+
+
+def random_hub_graphs(seed: int, count: int, n_lo: int = 300, n_hi: int = 6000, cost_hi: int = 1000):
+    """Medium general graphs for differential testing against the oracle: random
+    arcs plus one to four hubs (a node joined to a quarter to all of the others,
+    in both directions), a few large capacities, antiparallel
+    and zero-capacity arcs, several sources and sinks. Hubs exercise the engine's
+    hub chunks and inboxes and the cell solver's workgroup-wide items. Lower
+    bounds of 1 sit on some arcs out of sources. Costs are
+    non-negative, as in ksched's cost models (the reference's SSP assumes no
+    negative cycle). Four in five graphs get expensive source → hub → sink arcs
+    that make them feasible; the rest may be infeasible (then the solver must
+    say so)."""
+    rng = np.random.default_rng(seed)
+    for trial in range(count):
+        n = int(rng.integers(n_lo, n_hi))
+        mb = int(rng.integers(2 * n, 6 * n))
+        k = int(rng.integers(2, 40))
+        ends = rng.choice(n, 2 * k, replace=False) + 1
+        units = rng.integers(1, 200, k)
+        hubs = rng.choice(n, int(rng.integers(1, 5)), replace=False) + 1
+        src, dst = [], []
+        if rng.random() < 0.8:   # feasibility arcs first: they win the de-duplication below
+            src += [ends[:k], np.full(k, hubs[0])]
+            dst += [np.full(k, hubs[0]), ends[k:]]
+        nf = sum(x.shape[0] for x in src)
+        src.append(rng.integers(1, n + 1, mb))
+        dst.append(rng.integers(1, n + 1, mb))
+        for h in hubs:
+            deg = int(rng.integers(n // 4, n))
+            other = rng.choice(n, deg, replace=False) + 1
+            into = rng.random(deg) < 0.5
+            src.append(np.where(into, other, h))
+            dst.append(np.where(into, h, other))
+        src = np.concatenate(src).astype(np.int64)
+        dst = np.concatenate(dst).astype(np.int64)
+        keep = src != dst
+        src, dst = src[keep], dst[keep]
+        _, first = np.unique(src * (n + 1) + dst, return_index=True)
+        first.sort()
+        src, dst = src[first], dst[first]
+        m = src.shape[0]
+        feas = first < nf   # (first is sorted: kept feasibility arcs come first)
+        cap = rng.integers(0, 40, m)
+        big = rng.random(m) < 0.03
+        cap[big] = rng.integers(1000, 200000, int(big.sum()))
+        # lower bounds only on arcs out of sources (as ksched's running arcs out of a
+        # pinned task): anywhere else they mostly make a random graph infeasible
+        low = np.zeros(m, np.int64)
+        lb = np.isin(src, ends[:k]) & (cap > 0) & (rng.random(m) < 0.3)
+        low[lb] = 1
+        cost = rng.integers(0, cost_hi, m)
+        cap[feas] = 200
+        low[feas] = 0
+        cost[feas] = 50 * cost_hi
+        supply = np.zeros(n, np.int64)
+        supply[ends[:k] - 1] += units
+        supply[ends[k:] - 1] -= units
+        ntype = np.zeros(n, np.int32)
+        yield trial, gen.Graph(ntype, supply, src, dst, low, cap.astype(np.int64), cost.astype(np.int64))

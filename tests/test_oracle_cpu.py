@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from conftest import load_goldens, load_known_answers
-from graphs import graph_from_lists, random_graphs
+from graphs import graph_from_lists, random_graphs, random_hub_graphs
 from ksched_amd import gen
 from oracle import ko
 
@@ -130,6 +130,24 @@ def test_random_graphs_ssp_equals_cost_scaling():
             assert (c1, f1) == (c2, f2)
             assert ko.verify(g, fl1)[0] == 0 and ko.verify(g, fl2)[0] == 0
     assert feasible >= 10
+
+
+def test_hub_graphs_ssp_equals_cost_scaling():
+    """The GPU stress graphs (tests/test_gpu_stress.py): the two oracles agree on
+    every seed that test uses, and the mix holds feasible and infeasible graphs."""
+    feasible = infeasible = 0
+    for seed in (2026, 2027):
+        for _, g in random_hub_graphs(seed, 16):
+            st1, c1, f1, fl1, _ = ko.ssp(g)
+            st2, c2, f2, _ = ko.cost_scaling(g)
+            assert (st1 == 0) == (st2 == 0)
+            if st1 == 0:
+                feasible += 1
+                assert (c1, f1) == (c2, f2)
+                assert ko.verify(g, fl1)[0] == 0
+            else:
+                infeasible += 1
+    assert feasible >= 16 and infeasible >= 2
 
 
 def test_reference_path_config2():
