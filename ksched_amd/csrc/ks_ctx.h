@@ -24,8 +24,13 @@ struct ks_ctx {
     std::string err;
 
     std::vector<NodeRec> nodes;            // index = NodeID (slot 0 unused)
-    std::vector<uint32_t> epoch_of;        // per id: last apply that touched it
-    std::vector<int32_t> lastrm_of;        // per id: last REMOVE position in that apply
+    // per id, the stamps of the current apply in one record next to nothing else
+    // (a stream's node records touch them at scattered ids)
+    struct IdStamp {
+        uint32_t epoch = 0;     // last apply that touched the id
+        int32_t lastrm = -1;    // last REMOVE position in that apply
+    };
+    std::vector<IdStamp> ids;
     uint32_t epoch = 0;
     int64_t sum_others = 0;                // Σ supply of live non-sink nodes
     int64_t n_sinks = 0;

@@ -2907,6 +2907,23 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
                               long long* __restrict__ flows, long long* __restrict__ part,
                               long long* __restrict__ partf, long long* __restrict__ bal) {
     __shared__ long long sh[WPB];
+    // a hub's balance (the sink, the cluster aggregator: every arc into it adds to
+    // one word) is summed in LDS and added once per workgroup — one device atomic
+    // per arc on the same word serialised at the memory-side atomic unit (~0.1 ms
+    // per config-3 verify)
+    __shared__ long long hbal[HUB_LDS];
+    __shared__ int hslot[HUB_LDS];
+    if (threadIdx.x < HUB_LDS) hbal[threadIdx.x] = 0;
+    __syncthreads();
+    auto add_bal = [&](int x, int slot, long long v) {
+        const int h = x - g.hub_base;
+        if (h >= 0 && h < HUB_LDS) {
+            __hip_atomic_fetch_add(&hbal[h], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            hslot[h] = slot;   // (every writer stores the same slot)
+        } else {
+            atom_add(&bal[slot], v);
+        }
+    };
     long long csum = 0, fsum = 0;
     int bad = 0;
     for (long long i = blockIdx.x * (long long)BLK + threadIdx.x; i < hi; i += (long long)gridDim.x * BLK) {
@@ -2921,14 +2938,15 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
             continue;
         }
         const long long cp = cap[i] - low[i];
-        const long long rf = g.pos[p].rcap, rr = g.pos[g.pos[p].rev].rcap;
+        const Pos qf = g.pos[p], qr = g.pos[g.pos[p].rev];
+        const long long rf = qf.rcap, rr = qr.rcap;
         const long long f = cp - rf;
         if (rf < 0 || rr < 0 || f < 0 || f != rr) bad = 1;
         const long long fl = f + low[i];
         flows[i] = fl;
         if (fl) {   // conservation from the flows themselves (k_verify_balance), not from the excess words
-            atom_add(&bal[src[i]], -fl);
-            atom_add(&bal[dst[i]], fl);
+            add_bal(qr.head, src[i], -fl);   // (the reverse position's head is the arc's tail)
+            add_bal(qf.head, dst[i], fl);
         }
         csum += fl * cost[i];
         if (supply[dst[i]] < 0) fsum += fl;
@@ -2936,6 +2954,8 @@ __global__ void k_verify_arcs(DG g, int hi, const unsigned char* __restrict__ al
     }
     csum = block_sum(csum, sh);
     fsum = block_sum(fsum, sh);
+    __syncthreads();
+    if (threadIdx.x < HUB_LDS && hbal[threadIdx.x]) atom_add(&bal[hslot[threadIdx.x]], hbal[threadIdx.x]);
     if (threadIdx.x == 0) {
         part[blockIdx.x] = csum;
         partf[blockIdx.x] = fsum;
@@ -3716,11 +3736,20 @@ static int run_apply(EngineImpl& s, const NodeEdit* edits, size_t ne, const ks_d
     KS_CHECK(s.d_recs.ensure(std::max<size_t>(k, 1)));
     KS_CHECK(s.rec_ent.ensure(std::max<size_t>(k, 1)));
     KS_CHECK(s.d_edits.ensure(std::max<size_t>(ne, 1)));
+    const auto t0 = std::chrono::steady_clock::now();
     if (k) KS_CHECK(hipMemcpyAsync(s.d_recs.p, recs, k * sizeof(ks_delta), hipMemcpyHostToDevice, st));
     if (ne) KS_CHECK(hipMemcpyAsync(s.d_edits.p, edits, ne * sizeof(NodeEdit), hipMemcpyHostToDevice, st));
+    const auto t1 = std::chrono::steady_clock::now();
     KS_CHECK(store_apply(s.sd(), s.d_recs.p, (int)k, s.rec_ent.p, s.d_edits.p, (int)ne, st));
     rc = read_sctl(s, err);
     if (rc) return rc;
+    if (s.opts.log_cycles) {
+        const auto t2 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "apply: upload call %.3f ms (%.1f MB), store kernels + wait %.3f ms\n",
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     1e-6 * (double)(k * sizeof(ks_delta) + ne * sizeof(NodeEdit)),
+                     std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
     if (s.h_sctl->overflow & 12) {
         err = "store index or table exhausted";
         return KS_E_DEVICE;

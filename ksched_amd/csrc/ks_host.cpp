@@ -15,6 +15,8 @@
 // device resolves it in parallel.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 #include <new>
@@ -118,8 +120,7 @@ namespace {
 void ensure_node(ks_ctx* c, uint64_t id) {
     if (id >= c->nodes.size()) {
         c->nodes.resize(id + 1);
-        c->epoch_of.resize(id + 1, 0);
-        c->lastrm_of.resize(id + 1, -1);
+        c->ids.resize(id + 1);
     }
 }
 
@@ -192,8 +193,7 @@ ks_ctx* ks_create(int device, const ks_opts* opts) {
         return nullptr;
     }
     c->nodes.resize(1);
-    c->epoch_of.resize(1, 0);
-    c->lastrm_of.resize(1, -1);
+    c->ids.resize(1);
     return c;
 }
 
@@ -225,8 +225,7 @@ int ks_load_graph(ks_ctx* c, const ks_node* nodes, size_t n, const ks_arc* arcs,
         if (rc) return rc;
     }
     c->nodes.swap(fresh);
-    c->epoch_of.assign(maxid + 1, 0);
-    c->lastrm_of.assign(maxid + 1, -1);
+    c->ids.assign(maxid + 1, ks_ctx::IdStamp{});
     c->sum_others = c->n_sinks = c->n_tasks = 0;
     c->sink_id = 0;
     for (uint64_t id = 1; id <= maxid; ++id) account(c, id, c->nodes[id], 1);
@@ -256,16 +255,17 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     if (k && !d) return c->fail(KS_E_INVALID, "null delta array");
     if (k > (size_t)INT32_MAX) return c->fail(KS_E_RANGE, "delta stream too long");
     if (int g = store_guard(c)) return g;
+    const auto t_in = std::chrono::steady_clock::now();
     if (++c->epoch == 0) {   // epoch wrapped: forget old stamps
-        std::fill(c->epoch_of.begin(), c->epoch_of.end(), 0);
+        for (auto& st : c->ids) st.epoch = 0;
         c->epoch = 1;
     }
     std::vector<std::pair<uint64_t, NodeRec>> saved;   // first-touch state of every touched node
     auto touch = [&](uint64_t id) {
         ensure_node(c, id);
-        if (c->epoch_of[id] != c->epoch) {
-            c->epoch_of[id] = c->epoch;
-            c->lastrm_of[id] = -1;
+        if (c->ids[id].epoch != c->epoch) {
+            c->ids[id].epoch = c->epoch;
+            c->ids[id].lastrm = -1;
             saved.emplace_back(id, c->nodes[id]);
         }
     };
@@ -292,7 +292,7 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
                 }
                 touch(x.id);
                 c->nodes[x.id] = NodeRec{};
-                c->lastrm_of[x.id] = (int32_t)i;
+                c->ids[x.id].lastrm = (int32_t)i;
                 break;
             case KS_ADD_ARC:
                 rc = check_arc(c, x.src, x.dst, x.low, x.cap, x.cost);
@@ -335,7 +335,7 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
         ks::NodeEdit e;
         std::memset(&e, 0, sizeof(e));
         e.slot = (int32_t)(id - 1);
-        e.last_rm = c->lastrm_of[id];
+        e.last_rm = c->ids[id].lastrm;
         e.supply = now.alive ? now.excess : 0;
         e.alive = now.alive ? 1 : 0;
         e.type = (uint8_t)std::min<int32_t>(std::max<int32_t>(now.type, 0), 255);
@@ -346,7 +346,14 @@ int ks_apply_deltas(ks_ctx* c, const ks_delta* d, size_t k) {
     c->have_solution = false;
     c->map_fresh = false;
     c->flows_fresh = false;
+    const auto t_dev = std::chrono::steady_clock::now();
     rc = c->eng.apply(edits.data(), edits.size(), d, k, c->nslots(), c->err);
+    if (c->opts.log_cycles) {   // (ks_opts.log_cycles: the host's and the device's share of an apply)
+        const auto t_out = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "apply: %zu records, %zu node edits, host %.3f ms, device %.3f ms\n", k, edits.size(),
+                     std::chrono::duration<double, std::milli>(t_dev - t_in).count(),
+                     std::chrono::duration<double, std::milli>(t_out - t_dev).count());
+    }
     if (rc) {
         // the device may have applied part of the stream: the host goes back to its
         // state before the call (nodes and aggregates) and the store is marked

@@ -122,12 +122,12 @@ def _random_stream(rng, nodes, arcs, nrec):
     return np.array(recs, native.DELTA_DT)
 
 
-@pytest.mark.parametrize("seed", [5, 6])
-def test_random_delta_streams_match_full_graph(any_ctx, seed):
-    """Random delta streams (2,000 records a round, four rounds) on a hub graph:
-    after ks_apply_deltas the device solve equals the oracle on the full graph the
-    test-side restatement of the store builds (graphs.apply_deltas_to_arcs), or
-    both are infeasible."""
+@pytest.mark.parametrize("seed,nrec", [(5, 2000), (6, 2000), (7, 20000)])
+def test_random_delta_streams_match_full_graph(any_ctx, seed, nrec):
+    """Random delta streams (four rounds of 2,000 or of 20,000 records) on a hub
+    graph: after ks_apply_deltas the device solve equals the oracle on the full
+    graph the test-side restatement of the store builds
+    (graphs.apply_deltas_to_arcs), or both are infeasible."""
     from graphs import graph_from_store
     ctx = any_ctx
     rng = np.random.default_rng(seed)
@@ -139,7 +139,7 @@ def test_random_delta_streams_match_full_graph(any_ctx, seed):
     ctx.solve()
     solved = 0
     for rnd in range(4):
-        ctx.apply_deltas(_random_stream(rng, nodes, arcs, 2000))
+        ctx.apply_deltas(_random_stream(rng, nodes, arcs, nrec))
         h = graph_from_store(nodes, arcs)
         st, cost, fv, _, _ = ko.ssp(h)
         if st == 0:
@@ -152,3 +152,49 @@ def test_random_delta_streams_match_full_graph(any_ctx, seed):
                 ctx.solve()
             assert ei.value.code == native.KS_E_INFEASIBLE, f"round {rnd}"
     assert solved >= 2
+
+
+@pytest.mark.parametrize("bad", ["missing_endpoint", "self_loop", "remove_missing", "add_present"])
+def test_large_stream_error_rolls_back(ctx_engine, bad):
+    """A 20,000-record stream with one bad record near its end: the call fails,
+    nothing of the stream is applied (host or device: all or nothing, ks_host.cpp),
+    and the valid stream alone then solves as the oracle says."""
+    from graphs import graph_from_store
+    rng = np.random.default_rng(11)
+    g = next(g for _, g in random_hub_graphs(11, 20, n_lo=3000, n_hi=5000) if ko.ssp(g)[0] == 0)
+    nodes = {i + 1: [int(g.supply[i]), int(g.ntype[i])] for i in range(g.n)}
+    arcs = {(int(s), int(d)): (int(lo), int(c), int(k))
+            for s, d, lo, c, k in zip(g.src, g.dst, g.low, g.cap, g.cost)}
+    ctx_engine.load_graph(g)
+    ctx_engine.solve()
+    before = (dict((k, list(v)) for k, v in nodes.items()), dict(arcs))
+    good = _random_stream(rng, nodes, arcs, 20000)
+    alive = sorted(nodes)
+    row = np.zeros(1, native.DELTA_DT)
+    if bad == "missing_endpoint":   # (an id past every node ever present)
+        row[0]["kind"], row[0]["src"], row[0]["dst"], row[0]["cap"] = native.KS_ADD_ARC, max(nodes) + 10, alive[0], 1
+    elif bad == "self_loop":
+        row[0]["kind"], row[0]["src"], row[0]["dst"], row[0]["cap"] = native.KS_ADD_ARC, alive[0], alive[0], 1
+    elif bad == "remove_missing":
+        row[0]["kind"], row[0]["id"] = native.KS_REMOVE_NODE, max(nodes) + 10
+    else:
+        row[0]["kind"], row[0]["id"] = native.KS_ADD_NODE, alive[1]
+    stream = np.concatenate([good[:19000], row, good[19000:]])
+    with pytest.raises(native.KsError) as ei:
+        ctx_engine.apply_deltas(stream)
+    assert ei.value.code in (native.KS_E_INVALID, native.KS_E_RANGE)
+    # nothing applied: the original graph still solves as before
+    nodes, arcs = before
+    h = graph_from_store(nodes, arcs)
+    st, cost, fv, _, _ = ko.ssp(h)
+    r = ctx_engine.solve()
+    assert (r.cost, r.flow) == (cost, fv)
+    # and the valid stream alone applies and solves as the restatement says
+    ctx_engine.apply_deltas(good)
+    from graphs import apply_deltas_to_arcs
+    apply_deltas_to_arcs(nodes, arcs, good)
+    h = graph_from_store(nodes, arcs)
+    st, cost, fv, _, _ = ko.ssp(h)
+    if st == 0:
+        r = ctx_engine.solve()
+        assert (r.cost, r.flow) == (cost, fv)
