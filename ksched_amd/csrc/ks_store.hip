@@ -141,9 +141,33 @@ __device__ __forceinline__ void free_slots(const StoreDev& d, int s, bool fr) {
 // chunks from a per-node cursor (inserts and removals balance in a churning
 // cell, so hubs such as the cluster aggregator and the sink keep their slack
 // instead of forcing a CSR rebuild every few rounds).
+// used[x]++ for every active lane, one atomic per distinct x in the wave: the
+// lanes of one segment take consecutive values (new tasks' arcs into the cluster
+// aggregator and their unscheduled aggregators meet in one wave). The leaders are
+// found first and then add together, so the atomics' round trips overlap.
+__device__ __forceinline__ int wave_fill(int* used, int x) {
+    const int me = (int)__lane_id();
+    unsigned long long rem = __ballot(1);
+    int lead = me, rank = 0, cnt = 0;
+    while (rem) {
+        const int l = __ffsll((long long)rem) - 1;
+        const int xl = __shfl(x, l);
+        const unsigned long long same = __ballot(x == xl) & rem;
+        if ((same >> me) & 1) {
+            lead = l;
+            rank = __popcll(same & ((1ULL << me) - 1));
+        }
+        if (me == l) cnt = __popcll(same);
+        rem &= ~same;
+    }
+    int base = 0;
+    if (me == lead) base = atomicAdd(&used[x], cnt);
+    return __shfl(base, lead) + rank;
+}
+
 __device__ int claim_pos(const StoreDev& d, int x, int tag) {
     const int b = d.first[x], e = d.first[x + 1], cap = e - b;
-    const int ps = atomicAdd(&d.used[x], 1);
+    const int ps = wave_fill(d.used, x);
     if (ps < cap && atomicCAS(&d.ent[b + ps], -1, tag) == -1) return b + ps;
     constexpr int SCAN = 64;
     const int chunks = (cap + SCAN - 1) / SCAN;
@@ -203,6 +227,51 @@ __global__ void k_kill_scan(StoreDev d, int hi) {
         free_slots(d, s, fr);
         wave_count(&d.ctl->tombs, fr && h_tomb(d, e));
     }
+}
+
+// The same per removed node, over its own CSR segment (when the CSR is valid every
+// live arc has its two positions, and a removed node's arcs are in its segment):
+// one thread per node edit, the wave's lanes stepping through their segments
+// together (so the slot frees and counters of 64 nodes share each wave's atomics).
+// An arc whose two endpoints are both removed is handled once, from its tail's
+// segment. Config 4: ~5k removed tasks of a few positions each instead of a pass
+// over every arc slot.
+__device__ void kill_node_segment(const StoreDev& d, const NodeEdit* __restrict__ e, int ne, int i) {
+    int b = 0, len = 0;
+    if (i < ne) {
+        const NodeEdit x = e[i];
+        const int v = (x.last_rm >= 0 && x.was_alive) ? perm_of(d, x.slot) : -1;
+        if (v >= 0) {
+            b = d.first[v];
+            len = d.first[v + 1] - b;
+        }
+    }
+    int steps = len;
+    for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+    for (int j = 0; j < steps; ++j) {
+        bool fr = false;
+        int h = -1, s = 0;
+        const int t = j < len ? d.ent[b + j] : -1;
+        if (t >= 0) {
+            s = t >> 1;
+            const int sl = d.a_src[s], dl = d.a_dst[s];
+            const int lr = max(d.n_lastrm[sl], d.n_lastrm[dl]);
+            // (t odd: this node is the head; the tail's thread handles the arc when the tail is removed too)
+            if (d.a_alive[s] && lr >= 0 && (!(t & 1) || d.n_lastrm[sl] < 0)) {
+                h = h_find(d, arc_hkey((long long)sl + 1, (long long)dl + 1));
+                const int last = h >= 0 ? d.hlast[h] : -1;
+                kill_positions(d, s);
+                fr = last < lr;   // no record after the removal re-creates it
+            }
+        }
+        free_slots(d, s, fr);
+        wave_count(&d.ctl->tombs, fr && h_tomb(d, h));
+    }
+}
+
+__global__ void k_kill_nodes(StoreDev d, const NodeEdit* __restrict__ e, int ne) {
+    for (int i0 = blockIdx.x * SBLK; i0 < ne; i0 += gridDim.x * SBLK)   // (uniform per workgroup)
+        kill_node_segment(d, e, ne, i0 + (int)threadIdx.x);
 }
 
 __global__ void k_reset_used(StoreDev d, const NodeEdit* __restrict__ e, int ne) {
@@ -413,7 +482,10 @@ hipError_t store_apply(const StoreDev& d, const ks_delta* recs, int k, int* rec_
     if (ne) hipLaunchKernelGGL(k_mark_removed, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne, 1);
     if (k) hipLaunchKernelGGL(k_hash_records, dim3(grid(k)), dim3(SBLK), 0, st, d, recs, k, rec_ent);
     if (ne) {
-        hipLaunchKernelGGL(k_kill_scan, dim3(grid(d.acap)), dim3(SBLK), 0, st, d, d.acap);
+        if (d.csr_valid)
+            hipLaunchKernelGGL(k_kill_nodes, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne);
+        else
+            hipLaunchKernelGGL(k_kill_scan, dim3(grid(d.acap)), dim3(SBLK), 0, st, d, d.acap);
         hipLaunchKernelGGL(k_reset_used, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne);
         hipLaunchKernelGGL(k_node_edits, dim3(grid(ne)), dim3(SBLK), 0, st, d, edits, ne);
     }
