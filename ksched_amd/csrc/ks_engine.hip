@@ -2620,7 +2620,7 @@ __global__ void k_pr_apply(DG g, int packed) {
 constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
 [[maybe_unused]] constexpr int CYC_WALK = 1 << CYC_LOG;
 constexpr int CYC_SHORT = 7;              // a short search's doubling steps
-constexpr int CYC_EVERY = 8;              // refinement rounds between parent-graph searches
+constexpr int CYC_EVERY = 4;              // refinement rounds between parent-graph searches
 constexpr int CYC_PERIODS = 3;            // rounds + search periods per host check
 constexpr long long kPrcUnitsDiv = 4;   // an earlier finish (run_phase prc_early)
 
