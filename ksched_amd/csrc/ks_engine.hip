@@ -2620,7 +2620,11 @@ __global__ void k_pr_apply(DG g, int packed) {
 constexpr int CYC_LOG = 10;      // cycles up to 1,024 arcs are found
 [[maybe_unused]] constexpr int CYC_WALK = 1 << CYC_LOG;
 constexpr int CYC_SHORT = 7;              // a short search's doubling steps
-constexpr int CYC_EVERY = 4;              // refinement rounds between parent-graph searches
+// refinement rounds between parent-graph searches: 4 where the whole
+// search is one workgroup's LDS pass (small graphs: a search costs ~3 rounds),
+// 8 for the multi-launch search of large graphs (twice the launches for no gain)
+constexpr int CYC_EVERY_LDS = 4;
+constexpr int CYC_EVERY = 8;
 constexpr int CYC_PERIODS = 3;            // rounds + search periods per host check
 constexpr long long kPrcUnitsDiv = 4;   // an earlier finish (run_phase prc_early)
 
@@ -4877,7 +4881,7 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
             KS_HOT(cpv, k_cyc_push, ngrid, BLK, st, g, (const int*)J0, JMK, (const int*)onc, (const int*)R,
                    (const long long*)gsum, (const long long*)gcap, (const int*)gbad, bseq);
         };
-        // Batches of CYC_PERIODS × (CYC_EVERY rounds + a search), pipelined two deep:
+        // Batches of CYC_PERIODS × (CYC_EVERY[_LDS] rounds + a search), pipelined two deep:
         // batch b+1 is enqueued before the host waits for batch b's control snapshot
         // (k_prc_snap, into pinned memory), so the GPU does not idle through the
         // host's round trip (~27 µs per batch with a copy-engine read, r06 traces).
@@ -4894,7 +4898,8 @@ int Engine::solve(ks_result& res, bool warm, std::string& err) {
         auto enqueue_batch = [&](int slot) -> hipError_t {
             const int b = nb++;
             for (int per = 0; per < (b == 0 ? 1 : CYC_PERIODS) && used < cap; ++per) {
-                const int k = std::min(b == 0 ? 2 * CYC_EVERY : CYC_EVERY, cap - used);
+                const int every = lds_search ? CYC_EVERY_LDS : CYC_EVERY;
+                const int k = std::min(b == 0 ? 2 * every : every, cap - used);
                 bf_rounds(2, k, b == 0);
                 used += k;
                 search();
